@@ -1,0 +1,155 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU oracle for the DAC decoder (codes -> waveform).
+
+Functional fp32 restatement of the third-party decoder the reference calls
+(zonos/autoencoder.py:44-47 -> transformers DacModel.decode, modeling_dac.py:610-640;
+transformers 4.48.3 pinned by uv.lock:2063-2064, 5.15.0 in this image -- the decode
+arithmetic is the same in both). Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import it.
+
+Parity with transformers' DacModel is pinned by tests/test_oracle_golden.py against
+tests/golden/dac_*.npz, produced by tests/golden/make_golden.py from an actual
+``DacModel(DacConfig(sampling_rate=44100))`` loaded with the same synthetic weights.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+
+@dataclass
+class DacCfg:
+    """configuration_dac.py defaults for descript/dac_44khz."""
+    hidden_size: int = 1024          # latent channels
+    decoder_hidden_size: int = 1536
+    upsampling_ratios: tuple = (8, 8, 4, 2)
+    n_codebooks: int = 9
+    codebook_size: int = 1024
+    codebook_dim: int = 8
+    sampling_rate: int = 44100
+
+    @property
+    def hop_length(self):
+        return int(math.prod(self.upsampling_ratios))
+
+
+DAC_44KHZ = DacCfg()
+
+
+def dac_weight_shapes(c: DacCfg) -> dict:
+    """Decoder + quantizer-decode keys in transformers' DacModel state dict."""
+    s = {}
+    for k in range(c.n_codebooks):
+        q = f"quantizer.quantizers.{k}."
+        s[q + "codebook.weight"] = (c.codebook_size, c.codebook_dim)
+        s[q + "out_proj.weight"] = (c.hidden_size, c.codebook_dim, 1)
+        s[q + "out_proj.bias"] = (c.hidden_size,)
+    s["decoder.conv1.weight"] = (c.decoder_hidden_size, c.hidden_size, 7)
+    s["decoder.conv1.bias"] = (c.decoder_hidden_size,)
+    for i, st in enumerate(c.upsampling_ratios):
+        cin = c.decoder_hidden_size // 2 ** i
+        cout = c.decoder_hidden_size // 2 ** (i + 1)
+        b = f"decoder.block.{i}."
+        s[b + "snake1.alpha"] = (1, cin, 1)
+        s[b + "conv_t1.weight"] = (cin, cout, 2 * st)
+        s[b + "conv_t1.bias"] = (cout,)
+        for r in (1, 2, 3):
+            u = b + f"res_unit{r}."
+            s[u + "snake1.alpha"] = (1, cout, 1)
+            s[u + "conv1.weight"] = (cout, cout, 7)
+            s[u + "conv1.bias"] = (cout,)
+            s[u + "snake2.alpha"] = (1, cout, 1)
+            s[u + "conv2.weight"] = (cout, cout, 1)
+            s[u + "conv2.bias"] = (cout,)
+    cl = c.decoder_hidden_size // 2 ** len(c.upsampling_ratios)
+    s["decoder.snake1.alpha"] = (1, cl, 1)
+    s["decoder.conv2.weight"] = (1, cl, 7)
+    s["decoder.conv2.bias"] = (1,)
+    return s
+
+
+def make_dac_weights(c: DacCfg = DAC_44KHZ, seed: int = 0, gain: float = 0.5) -> dict:
+    """Seeded synthetic DAC weights. Variance-preserving init (std = gain/sqrt(fan_in)) so the
+    waveform is not near-silent (random HF init gives RMS ~5e-3), which would make
+    an RMS-error criterion vacuous."""
+    out = {}
+    for idx, (k, shape) in enumerate(dac_weight_shapes(c).items()):
+        g = torch.Generator().manual_seed(seed * 1_000_003 + 7919 * idx + 17)
+        if k.endswith("alpha"):
+            t = 0.5 + torch.rand(shape, generator=g)
+        elif k.endswith("bias"):
+            t = 0.05 * torch.randn(shape, generator=g)
+        elif k.endswith("codebook.weight"):
+            t = torch.randn(shape, generator=g)
+        elif "conv_t1" in k:
+            cin, cout, ks = shape
+            t = torch.randn(shape, generator=g) * (gain / math.sqrt(cin * 2))
+        else:
+            fan_in = shape[1] * shape[2]
+            t = torch.randn(shape, generator=g) * (gain / math.sqrt(fan_in))
+        out[k] = t.float()
+    return out
+
+
+def snake(x, alpha):
+    """Snake1d.forward (modeling_dac.py:95-100): x + 1/(a+1e-9) * sin(a x)^2."""
+    shape = x.shape
+    x = x.reshape(shape[0], shape[1], -1)
+    x = x + (alpha + 1e-9).reciprocal() * torch.sin(alpha * x).pow(2)
+    return x.reshape(shape)
+
+
+def from_codes(W, c: DacCfg, codes: torch.Tensor) -> torch.Tensor:
+    """DacResidualVectorQuantizer.from_codes (modeling_dac.py:347-371): sum_k out_proj_k(codebook_k[c_k])."""
+    z = 0.0
+    for k in range(codes.shape[1]):
+        q = f"quantizer.quantizers.{k}."
+        lat = F.embedding(codes[:, k, :], W[q + "codebook.weight"]).transpose(1, 2)
+        z = z + F.conv1d(lat, W[q + "out_proj.weight"], W[q + "out_proj.bias"])
+    return z
+
+
+def res_unit(W, p, x, dil):
+    """DacResidualUnit.forward (modeling_dac.py:175-209)."""
+    y = F.conv1d(snake(x, W[p + "snake1.alpha"]), W[p + "conv1.weight"], W[p + "conv1.bias"],
+                 dilation=dil, padding=3 * dil)
+    y = F.conv1d(snake(y, W[p + "snake2.alpha"]), W[p + "conv2.weight"], W[p + "conv2.bias"])
+    pad = (x.shape[-1] - y.shape[-1]) // 2
+    if pad > 0:
+        x = x[..., pad:-pad]
+    return x + y
+
+
+def decoder(W, c: DacCfg, z: torch.Tensor) -> torch.Tensor:
+    """DacDecoder.forward (modeling_dac.py:431-441) with DacDecoderBlock (236-264)."""
+    x = F.conv1d(z, W["decoder.conv1.weight"], W["decoder.conv1.bias"], padding=3)
+    for i, st in enumerate(c.upsampling_ratios):
+        b = f"decoder.block.{i}."
+        x = snake(x, W[b + "snake1.alpha"])
+        x = F.conv_transpose1d(x, W[b + "conv_t1.weight"], W[b + "conv_t1.bias"], stride=st,
+                               padding=math.ceil(st / 2))
+        for r, dil in ((1, 1), (2, 3), (3, 9)):
+            x = res_unit(W, b + f"res_unit{r}.", x, dil)
+    x = snake(x, W["decoder.snake1.alpha"])
+    x = F.conv1d(x, W["decoder.conv2.weight"], W["decoder.conv2.bias"], padding=3)
+    return torch.tanh(x)
+
+
+def decode(W, c: DacCfg, codes: torch.Tensor) -> torch.Tensor:
+    """DACAutoencoder.decode on CPU (autoencoder.py:44-47, fp32): codes [B,9,T] -> [B,1,hop*T]."""
+    assert codes.shape[1] == c.n_codebooks
+    with torch.no_grad():
+        return decoder(W, c, from_codes(W, c, codes)).squeeze(1).unsqueeze(1).float()
+
+
+def decode_list(W, c: DacCfg, codes_list) -> list:
+    """The decode half of codes_to_wavs (autoencoder.py:219-226): one utterance at a time."""
+    out = []
+    for x in codes_list:
+        x = x.unsqueeze(0) if x.dim() == 2 else x
+        if x.shape[2] == 0:
+            continue
+        out.append(decode(W, c, x).squeeze(0))
+    return out

@@ -1,0 +1,314 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Run in the build container only (needs /root/reference):
+    python tests/golden/make_golden.py
+
+The reference package is imported from /root/reference with import-only stubs for
+the front-end libraries that are absent here (torchaudio, inflect, kanjize,
+phonemizer, sudachipy) -- they are not on the decode path. The reference's DAC
+wrapper normally fetches "descript/dac_44khz" by name (autoencoder.py:15); offline we
+build transformers' DacModel locally and load the same synthetic weights the oracle
+uses (oracle.dac_ref.make_dac_weights).
+
+Sampling noise: the reference draws Exp(1) noise from torch's generator in
+zonos.sampling.multinomial (sampling.py:26-28). We replace that one function with
+one that takes the engine's counter-based stream (oracle.philox.exp_noise), keyed by
+(step, draw) exactly as the engine keys it, so seeded sampling is comparable.
+Everything else runs unmodified reference code.
+
+Outputs are small .npz files (inputs + expected outputs only); weights are
+regenerated deterministically from their seeds by oracle.zonos_ref.make_weights /
+oracle.dac_ref.make_dac_weights, and a checksum of them is stored for verification.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+import transformers.models.dac.modeling_dac  # noqa: E402,F401  (before the torchaudio stub)
+from transformers import DacConfig, DacModel  # noqa: E402
+
+
+class _Any:
+    def __init__(self, *a, **k): pass
+    def __call__(self, *a, **k): return _Any()
+    def __getattr__(self, n): return _Any()
+
+
+class _Stub(types.ModuleType):
+    def __getattr__(self, n):
+        if n.startswith("__"):
+            raise AttributeError(n)
+        return _Any
+
+
+for _m in ["torchaudio", "torchaudio.functional", "inflect", "kanjize", "phonemizer",
+           "phonemizer.backend", "sudachipy"]:
+    sys.modules[_m] = _Stub(_m)
+sys.path.insert(0, "/root/reference")
+
+import zonos.autoencoder as zae  # noqa: E402
+import zonos.model as zm  # noqa: E402
+import zonos.sampling as zs  # noqa: E402
+from zonos.backbone import BACKBONES  # noqa: E402
+from zonos.codebook_pattern import apply_delay_pattern, revert_delay_pattern  # noqa: E402
+from zonos.config import ZonosConfig  # noqa: E402
+
+from oracle import dac_ref, zonos_ref  # noqa: E402
+from oracle.philox import exp_noise  # noqa: E402
+
+TINY = zonos_ref.BackboneCfg(d_model=256, n_layer=2, n_heads=2, n_kv=1, d_ff=512)
+TINY_DAC = dac_ref.DacCfg(hidden_size=64, decoder_hidden_size=64, upsampling_ratios=(4, 2))
+
+
+def wsum(W: dict) -> str:
+    h = hashlib.sha256()
+    for k in sorted(W):
+        h.update(k.encode())
+        h.update(W[k].float().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+# ---------------------------------------------------------------- noise injection
+class NoiseCtl:
+    seed = 0
+    step = 0
+    draw = 0
+    row_base = 0
+
+
+def _patched_multinomial(input, num_samples, replacement=False, *, generator=None):
+    assert num_samples == 1
+    B, K, V = input.shape
+    q = torch.from_numpy(exp_noise(NoiseCtl.seed, NoiseCtl.step, NoiseCtl.draw, B, K, V, NoiseCtl.row_base))
+    return torch.argmax(input / q, dim=-1, keepdim=True).to(torch.int64)
+
+
+zs.multinomial = _patched_multinomial
+_orig_sample = zm.sample_from_logits
+_last_off = {"v": None}
+
+
+def _tracking_sample(logits, generated_tokens=None, **kw):
+    """Map each reference sampler call to the engine's (step, draw) key."""
+    if generated_tokens is None:
+        NoiseCtl.step, NoiseCtl.draw = 0, 0
+        _last_off["v"] = None
+    else:
+        off = generated_tokens.shape[2]
+        if _last_off["v"] == off:
+            NoiseCtl.draw = 1
+        else:
+            NoiseCtl.step += 1
+            NoiseCtl.draw = 0
+        _last_off["v"] = off
+    return _orig_sample(logits, generated_tokens=generated_tokens, **kw)
+
+
+zm.sample_from_logits = _tracking_sample
+
+
+# ---------------------------------------------------------------- reference model build
+def _dac_init(self):
+    self.dac = DacModel(DacConfig(sampling_rate=44100))
+    self.dac.eval().requires_grad_(False)
+    self.codebook_size = self.dac.config.codebook_size
+    self.num_codebooks = self.dac.quantizer.n_codebooks
+    self.sampling_rate = self.dac.config.sampling_rate
+
+
+zae.DACAutoencoder.__init__ = _dac_init
+
+
+def build_ref_model(cfg, W):
+    zc = ZonosConfig.from_dict(cfg.to_zonos_config())
+    model = zm.Zonos(zc, BACKBONES["torch"]).to(torch.bfloat16)
+    sd = model.state_dict()
+    for k, v in W.items():
+        sd[k] = v
+    model.load_state_dict(sd)   # post-hook pads heads 1025 -> 1026 (model.py:46-51)
+    model.eval()
+    return model
+
+
+def run_generate(model, cond, prefix, B, max_new, sp, seed, logits_steps=0):
+    NoiseCtl.seed = seed
+    rec = []
+    orig = model._compute_logits
+
+    def rec_logits(*a, **k):
+        out = orig(*a, **k)
+        if len(rec) < logits_steps:
+            rec.append(out.clone())
+        return out
+
+    model._compute_logits = rec_logits
+    out = model.generate(cond, audio_prefix_codes=prefix, max_new_tokens=max_new, cfg_scale=2.0,
+                         batch_size=B, sampling_params=sp, progress_bar=False, disable_torch_compile=True)
+    model._compute_logits = orig
+    return out, rec
+
+
+def pack_codes(lst):
+    T = max(int(x.shape[1]) for x in lst) if lst else 0
+    arr = np.full((len(lst), 9, T), -1, dtype=np.int16)
+    lens = np.zeros(len(lst), dtype=np.int32)
+    for i, x in enumerate(lst):
+        arr[i, :, :x.shape[1]] = x.numpy()
+        lens[i] = x.shape[1]
+    return arr, lens
+
+
+GEN_CASES = {
+    "greedy": dict(sp=dict(temperature=0.0, top_p=0, top_k=0, min_p=0, linear=0.0, conf=0.0, quad=0.0,
+                           repetition_penalty=1.0, repetition_penalty_window=2), eos_bias=0.0, logits=6),
+    "greedy_rep": dict(sp=dict(temperature=0.0, top_p=0, top_k=0, min_p=0, linear=0.0, conf=0.0, quad=0.0,
+                               repetition_penalty=2.5, repetition_penalty_window=8), eos_bias=0.0, logits=0),
+    "sampled_cli": dict(sp=dict(top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0,
+                                repetition_penalty=2.5, repetition_penalty_window=8, temperature=1.0),
+                        eos_bias=0.0, logits=0),
+    "sampled_knobs": dict(sp=dict(top_p=0.9, top_k=50, min_p=0.05, linear=0.0, conf=0.0, quad=0.0,
+                                  repetition_penalty=1.5, repetition_penalty_window=4, temperature=0.8),
+                          eos_bias=0.0, logits=0),
+    "eos_greedy": dict(sp=dict(temperature=0.0, top_p=0, top_k=0, min_p=0, linear=0.0, conf=0.0, quad=0.0,
+                               repetition_penalty=1.0, repetition_penalty_window=2), eos_bias=10.0, logits=0),
+    "eos_sampled": dict(sp=dict(top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0,
+                                repetition_penalty=2.5, repetition_penalty_window=8, temperature=1.0),
+                        eos_bias=10.0, logits=0),
+}
+GEN_B, GEN_LC, GEN_P, GEN_NEW, HEAD_SCALE = 3, 12, 4, 40, 4.0
+
+
+def make_generate_fixtures():
+    cond = zonos_ref.synthetic_conditioning(GEN_B, GEN_LC, TINY.d_model, seed=1)
+    prefix = zonos_ref.synthetic_prefix_codes(GEN_B, GEN_P, seed=3)
+    for name, case in GEN_CASES.items():
+        W = zonos_ref.make_weights(TINY, seed=0, head_scale=HEAD_SCALE, eos_bias=case["eos_bias"])
+        model = build_ref_model(TINY, W)
+        seed = 1234
+        out, rec = run_generate(model, cond, prefix, GEN_B, GEN_NEW, case["sp"], seed, case["logits"])
+        # oracle cross-check right here (same container, same torch): must be bit-identical.
+        trace = {}
+        Wp = zonos_ref.pad_heads(W, TINY)
+        out_o = zonos_ref.generate(Wp, TINY, cond, prefix, GEN_NEW, 2.0, GEN_B, case["sp"], seed=seed,
+                                   trace=trace)
+        same = all(torch.equal(a, b) for a, b in zip(out, out_o)) and len(out) == len(out_o)
+        codes, lens = pack_codes(out)
+        print(f"[gen:{name}] lens={lens.tolist()} oracle_match={same}")
+        assert same, f"oracle diverges from reference on {name}"
+        d = dict(codes=codes, lens=lens, cond=cond.view(torch.int16).numpy(), prefix=prefix.numpy().astype(np.int16),
+                 seed=np.int64(seed), wsum=np.array(wsum(W)), eos_bias=np.float32(case["eos_bias"]),
+                 head_scale=np.float32(HEAD_SCALE), max_new=np.int32(GEN_NEW),
+                 delayed=trace["delayed"].numpy().astype(np.int16), offset=np.int32(trace["offset"]))
+        for k, v in case["sp"].items():
+            d["sp_" + k] = np.float64(v)
+        if rec:
+            d["logits"] = torch.stack(rec).numpy().astype(np.float32)
+        np.savez_compressed(os.path.join(HERE, f"gen_{name}.npz"), **d)
+
+
+SAMPLER_CASES = [
+    dict(temperature=0.0, repetition_penalty=1.0, repetition_penalty_window=2),
+    dict(temperature=0.0, repetition_penalty=2.5, repetition_penalty_window=8),
+    dict(temperature=1.0, repetition_penalty=1.0, repetition_penalty_window=2),
+    dict(temperature=0.7, repetition_penalty=3.0, repetition_penalty_window=2),
+    dict(temperature=1.0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5, repetition_penalty_window=8),
+    dict(temperature=1.0, linear=0.5, conf=0.2, quad=0.3, repetition_penalty=1.0, repetition_penalty_window=2),
+    dict(temperature=1.0, top_p=0.8, repetition_penalty=1.0, repetition_penalty_window=2),
+    dict(temperature=1.0, top_k=20, repetition_penalty=1.0, repetition_penalty_window=2),
+    dict(temperature=1.0, top_k=1, repetition_penalty=1.0, repetition_penalty_window=2),
+    dict(temperature=1.0, min_p=0.1, repetition_penalty=1.0, repetition_penalty_window=2),
+    dict(temperature=0.9, top_p=0.95, top_k=64, min_p=0.02, linear=0.6, conf=0.3, quad=0.1,
+         repetition_penalty=2.0, repetition_penalty_window=6),
+]
+
+
+def make_sampler_fixtures():
+    g = torch.Generator().manual_seed(11)
+    B, K, V, L = 4, 9, 1026, 12
+    out = {}
+    for ci, sp in enumerate(SAMPLER_CASES):
+        logits = torch.randn(B, K, V, generator=g) * 3.0
+        logits[..., 1025:] = -torch.inf
+        logits[1, 3, 5] = -torch.inf
+        gen = torch.randint(0, 1026, (B, K, L), generator=g)
+        gen[..., -3:] = torch.argmax(logits, dim=-1, keepdim=True)   # make the penalty bite
+        rp = torch.tensor([sp["repetition_penalty"], 1.0, sp["repetition_penalty"], sp["repetition_penalty"]])
+        NoiseCtl.seed, NoiseCtl.step, NoiseCtl.draw = 77, ci + 1, 0
+        kw = {k: v for k, v in sp.items() if k != "repetition_penalty"}
+        tok = zs.sample_from_logits(logits.clone(), generated_tokens=gen, repetition_penalty=rp.clone(), **kw)
+        # oracle
+        q = torch.from_numpy(exp_noise(77, ci + 1, 0, B, K, V))
+        tok_o = zonos_ref.sample(logits.clone(), q, generated_tokens=gen, repetition_penalty=rp.clone(), **kw)
+        assert torch.equal(tok, tok_o), f"sampler oracle mismatch case {ci}"
+        out[f"logits_{ci}"] = logits.numpy()
+        out[f"gen_{ci}"] = gen.numpy().astype(np.int16)
+        out[f"rp_{ci}"] = rp.numpy()
+        out[f"tok_{ci}"] = tok.squeeze(-1).numpy().astype(np.int16)
+        for k, v in sp.items():
+            out[f"sp_{ci}_{k}"] = np.float64(v)
+    out["n_cases"] = np.int32(len(SAMPLER_CASES))
+    out["seed"] = np.int64(77)
+    np.savez_compressed(os.path.join(HERE, "sampler.npz"), **out)
+    print(f"[sampler] {len(SAMPLER_CASES)} cases ok")
+
+
+def make_delay_fixtures():
+    g = torch.Generator().manual_seed(5)
+    codes = torch.randint(0, 1024, (2, 9, 7), generator=g)
+    codes[1, :, 4:] = -1
+    d = apply_delay_pattern(codes, 1025)
+    r = revert_delay_pattern(d)
+    assert torch.equal(d, zonos_ref.apply_delay(codes)) and torch.equal(r, zonos_ref.revert_delay(d))
+    np.savez_compressed(os.path.join(HERE, "delay.npz"), codes=codes.numpy().astype(np.int16),
+                        delayed=d.numpy().astype(np.int16), reverted=r.numpy().astype(np.int16))
+    print("[delay] ok")
+
+
+def make_dac_fixtures():
+    for name, c, T, seed in (("dac_tiny", TINY_DAC, (20, 13), 4), ("dac_44k", dac_ref.DAC_44KHZ, (12, 7), 0)):
+        W = dac_ref.make_dac_weights(c, seed=seed)
+        hf = DacModel(DacConfig(sampling_rate=44100, hidden_size=c.hidden_size,
+                                decoder_hidden_size=c.decoder_hidden_size,
+                                upsampling_ratios=list(c.upsampling_ratios),
+                                n_codebooks=c.n_codebooks, codebook_size=c.codebook_size,
+                                codebook_dim=c.codebook_dim))
+        sd = hf.state_dict()
+        for k, v in W.items():
+            assert sd[k].shape == v.shape, (k, sd[k].shape, v.shape)
+            sd[k] = v
+        hf.load_state_dict(sd)
+        hf.eval()
+        g = torch.Generator().manual_seed(seed + 100)
+        codes = torch.randint(0, c.codebook_size, (2, c.n_codebooks, T[0]), generator=g)
+        short = codes[1:, :, :T[1]].clone()
+        with torch.no_grad():
+            wav_b = hf.decode(audio_codes=codes).audio_values.unsqueeze(1).float()   # autoencoder.py:47 (CPU)
+            wav_s = hf.decode(audio_codes=short).audio_values.unsqueeze(1).float()
+        o_b = dac_ref.decode(W, c, codes)
+        o_s = dac_ref.decode(W, c, short)
+        eb = (o_b - wav_b).abs().max().item()
+        es = (o_s - wav_s).abs().max().item()
+        print(f"[{name}] rms={wav_b.pow(2).mean().sqrt().item():.4f} oracle max|d| batch={eb:.2e} short={es:.2e}")
+        assert eb < 1e-5 and es < 1e-5
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), codes=codes.numpy().astype(np.int16),
+                            wav=wav_b.numpy(), wav_short=wav_s.numpy(), short_len=np.int32(T[1]),
+                            seed=np.int64(seed), wsum=np.array(wsum(W)),
+                            cfg=np.array([c.hidden_size, c.decoder_hidden_size, *c.upsampling_ratios]))
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    make_delay_fixtures()
+    make_sampler_fixtures()
+    make_generate_fixtures()
+    make_dac_fixtures()

@@ -1,0 +1,85 @@
+"""CPU: the oracle (oracle/) against golden vectors produced by the REFERENCE itself
+(tests/golden/make_golden.py). These pin the checker before it is trusted."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dac_ref, zonos_ref
+from oracle.philox import exp_noise, philox4x32_10
+
+from .golden_util import GEN_CASES, TINY, TINY_DAC, load_gen_case, wsum
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_philox_known_answers():
+    # Random123 KAT vectors for philox4x32-10
+    assert [int(x) for x in philox4x32_10(0, 0, 0, 0, 0, 0)] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    assert [int(x) for x in philox4x32_10(*([0xFFFFFFFF] * 6))] == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    assert [int(x) for x in philox4x32_10(0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, 0xa4093822,
+                                          0x299f31d0)] == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def test_noise_is_exponential():
+    q = exp_noise(5, 1, 0, 8, 9, 1026)
+    assert q.dtype == np.float32 and q.min() > 0
+    assert abs(float(q.mean()) - 1.0) < 0.02
+    # shard invariance: rows [4,8) drawn with row_base=4 equal the full draw
+    assert np.array_equal(exp_noise(5, 1, 0, 4, 9, 1026, row_base=4), q[4:])
+
+
+def test_delay_pattern_golden():
+    d = np.load(os.path.join(G, "delay.npz"))
+    codes = torch.from_numpy(d["codes"].astype(np.int64))
+    dl = zonos_ref.apply_delay(codes)
+    assert np.array_equal(dl.numpy(), d["delayed"])
+    assert np.array_equal(zonos_ref.revert_delay(dl).numpy(), d["reverted"])
+    assert torch.equal(zonos_ref.revert_delay(dl), codes)
+
+
+def test_sampler_golden():
+    d = np.load(os.path.join(G, "sampler.npz"))
+    for ci in range(int(d["n_cases"])):
+        sp = {k[len(f"sp_{ci}_"):]: float(d[k]) for k in d.files if k.startswith(f"sp_{ci}_")}
+        sp["top_k"] = int(sp.get("top_k", 0))
+        sp["repetition_penalty_window"] = int(sp["repetition_penalty_window"])
+        sp.pop("repetition_penalty")
+        logits = torch.from_numpy(d[f"logits_{ci}"])
+        B, K, V = logits.shape
+        q = torch.from_numpy(exp_noise(int(d["seed"]), ci + 1, 0, B, K, V))
+        tok = zonos_ref.sample(logits, q, generated_tokens=torch.from_numpy(d[f"gen_{ci}"].astype(np.int64)),
+                               repetition_penalty=torch.from_numpy(d[f"rp_{ci}"]), **sp)
+        assert np.array_equal(tok.squeeze(-1).numpy(), d[f"tok_{ci}"]), f"case {ci}"
+
+
+@pytest.mark.parametrize("name", list(GEN_CASES))
+def test_generate_golden(name):
+    c = load_gen_case(name)
+    assert wsum(c["W_raw"]) == c["wsum"], "synthetic weights are not reproducible on this host"
+    trace = {}
+    out = zonos_ref.generate(c["W"], TINY, c["cond"], c["prefix"], c["max_new"], 2.0, c["B"], c["sp"],
+                             seed=c["seed"], trace=trace)
+    assert [int(x.shape[1]) for x in out] == c["lens"].tolist()
+    for i, x in enumerate(out):
+        assert np.array_equal(x.numpy(), c["codes"][i, :, :c["lens"][i]]), f"row {i}"
+    assert np.array_equal(trace["delayed"].numpy(), c["delayed"])
+    if c["logits"] is not None:
+        got = torch.stack(trace["logits"][:len(c["logits"])]).numpy()
+        assert np.array_equal(got, c["logits"])
+
+
+@pytest.mark.parametrize("name", ["dac_tiny", "dac_44k"])
+def test_dac_golden(name):
+    d = np.load(os.path.join(G, f"{name}.npz"))
+    c = TINY_DAC if name == "dac_tiny" else dac_ref.DAC_44KHZ
+    W = dac_ref.make_dac_weights(c, seed=int(d["seed"]))
+    assert wsum(W) == str(d["wsum"])
+    codes = torch.from_numpy(d["codes"].astype(np.int64))
+    got = dac_ref.decode(W, c, codes)
+    assert (got - torch.from_numpy(d["wav"])).abs().max().item() < 1e-5
+    L = int(d["short_len"])
+    got_s = dac_ref.decode_list(W, c, [codes[1, :, :L]])[0]
+    assert (got_s - torch.from_numpy(d["wav_short"][0])).abs().max().item() < 1e-5
