@@ -1,0 +1,191 @@
+/* zonos_hip.h -- C ABI of libzonos_hip.so, the MI355X (gfx950) engine for the Zonos
+ * decode hot path: generate() autoregressive DAC-token decode and the DAC decoder.
+ *
+ * Conventions
+ *   - Plain C types only: device pointers are passed as `void*`/typed pointers obtained
+ *     from the caller's allocator (torch.Tensor.data_ptr() in zonos_amd), sizes as int.
+ *   - Every call is asynchronous on the `stream` argument (a hipStream_t passed as void*;
+ *     NULL = default stream) and returns 0 on success, <0 on error; the message is
+ *     available from zk_last_error() (thread-local). No C++ exception crosses the ABI.
+ *   - bf16 tensors are raw uint16 bit patterns (torch.bfloat16 storage).
+ *   - The reference interface each entry point replaces is cited as file:line relative
+ *     to the coezbek/Zonos checkout (modeling_dac.py = transformers' DAC).
+ */
+#ifndef ZONOS_HIP_H
+#define ZONOS_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ library */
+int zk_version(void);                 /* ABI version (monotonic) */
+const char* zk_last_error(void);      /* thread-local message of the last failing call */
+int zk_device_sync(void);             /* hipDeviceSynchronize + error check */
+
+/* ------------------------------------------------------------------ sampling
+ * Mirrors sample_from_logits (zonos/sampling.py:232-328) incl.
+ * modify_logit_for_repetition_penalty (131-169), apply_unified (54-75),
+ * apply_top_p (96-111), apply_top_k (77-93), apply_min_p (114-128) and the
+ * exponential-race multinomial (11-33). The Exp(1) noise is the engine's
+ * Philox4x32-10 stream keyed by (seed, step, draw, row_base+b, codebook, token);
+ * see oracle/philox.py for the exact definition. */
+typedef struct zk_sampling_params {
+    float temperature;        /* 0 => argmax (sampling.py:325-326) */
+    float top_p;              /* 0 disables */
+    float min_p;              /* 0 disables */
+    float linear, conf, quad; /* unified sampler; linear<=0 disables */
+    int32_t top_k;            /* 0 disables */
+    int32_t rp_window;        /* repetition_penalty_window */
+    float cfg_scale;          /* classifier-free guidance scale (model.py:112-114) */
+    int32_t force_full_length;/* benchmark mode: cb0 EOS logit forced to -inf every step */
+} zk_sampling_params;
+
+/* Standalone sampler over fp32 logits [B][K][V] (already CFG-combined).
+ * generated: int64 [B][K][gen_stride] token history (the reference passes
+ *            delayed_codes[..., :offset]); the last rp_window of the first `gen_len`
+ *            columns are penalised; NULL => no repetition penalty (prefill call).
+ * rp:        float [B] per-row repetition penalty (model.py:342,356).
+ * out:       int64 [B][K] sampled tokens. */
+int zk_sample_logits(const float* logits, int B, int K, int V,
+                     const int64_t* generated, int gen_stride, int gen_len, const float* rp,
+                     const zk_sampling_params* sp, uint64_t seed, int step, int draw, int row_base,
+                     int64_t* out, void* stream);
+
+/* Delay pattern (zonos/codebook_pattern.py:5-12). codes int64 [B][K][T] ->
+ * delayed int64 [B][K][T+K]; revert: delayed [B][K][L] -> codes [B][K][L-K]. */
+int zk_delay_apply(const int64_t* codes, int B, int K, int T, int64_t mask_token,
+                   int64_t* delayed, void* stream);
+int zk_delay_revert(const int64_t* delayed, int B, int K, int L, int64_t* codes, void* stream);
+
+/* ------------------------------------------------------------------ backbone building blocks
+ * (zonos/backbone/_torch.py). All activations bf16 row-major. */
+
+/* embed_codes (model.py:97-98) + the CFG row duplication (model.py:141) + the first
+ * LayerNorm of layer 0 (_torch.py:100). ids: int64 codes read at ids[b*ids_bstride +
+ * k*ids_kstride + col] with col = t + (col_dev ? *col_dev + col_add : 0), t in [0,S).
+ * Output row r*out_S + out_t0 + t for r in [0, rows_dup*B) uses utterance r % B.
+ * x_out = embedding sum; if ln_w != NULL also xn_out = LayerNorm(x_out).
+ * skip (nullable, device int32): when *skip != 0 the kernel does nothing (generation done). */
+int zk_embed_codes(const int64_t* ids, int B, int S, int K, long ids_bstride, long ids_kstride,
+                   const int32_t* col_dev, int col_add, const void* emb, int V, int D, int rows_dup,
+                   void* x_out, int out_S, int out_t0, const void* ln_w, const void* ln_b, float eps,
+                   void* xn_out, const int32_t* skip, void* stream);
+
+/* y = LayerNorm(x) (nn.LayerNorm with bias, _torch.py:88,90,62), rows x D. */
+int zk_layernorm(const void* x, const void* w, const void* b, float eps, int rows, int D,
+                 void* y, void* stream);
+
+/* x_out = bf16(x_in + bf16(sum_s part[s])) ; xn = LayerNorm(x_out) (_torch.py:100-101).
+ * part: fp32 [nsplit][rows][D] split-K slabs of the preceding projection. */
+int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, const void* b,
+                float eps, int rows, int D, void* x_out, void* xn_out, const int32_t* skip, void* stream);
+
+/* C = A[M][K] . W[N][K]^T (nn.Linear, bias-free). bf16 in, fp32 accumulation (MFMA).
+ * mode 0: fp32 split-K slabs Cpart[split][M][N] (nsplit = K-split count);
+ * mode 1: SwiGLU epilogue for FeedForward fc1 (_torch.py:147,151-152): W rows must be
+ *         in the engine's interleaved order (zk_permute_fc1) and Cout is bf16 [M][N/2].
+ * lda = row stride of A in elements (lets the heads GEMM read only the last token). */
+int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
+                 float* Cpart, void* Cout, const int32_t* skip, void* stream);
+/* fc1 weight [2F][D] (rows: F "y" then F "gate") -> interleaved groups of 8 y + 8 gate rows. */
+int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream);
+
+/* Sum split-K slabs of in_proj, round to bf16, apply interleaved RoPE to q and k
+ * (apply_rotary_emb _torch.py:18-30; positions pos0 + t (+ *pos_dev if non-NULL);
+ * freqs = precompute_freqs_cis table [16384][hd/2][2], _torch.py:9-15), store q
+ * [rows][H*hd] and write k, v into the layer cache (_update_kv_cache _torch.py:33-49).
+ * Cache layout (engine-owned): K [R][Hkv][Smax][hd], V^T [R][Hkv][hd][Smax].
+ * v_rows (nullable): also write V as [R][Hkv][S][hd] (prefill scratch).
+ * rows = R*S tokens ordered r*S + t. */
+int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv, int hd,
+                const float* freqs, int pos0, const int32_t* pos_dev,
+                void* q_out, void* k_cache, void* vt_cache, int Smax, void* v_rows,
+                const int32_t* skip, void* stream);
+
+/* Scaled-dot-product attention over the cache (F.scaled_dot_product_attention,
+ * _torch.py:136; GQA, scale 1/sqrt(hd)).
+ * decode: one query per row, keys [0, ctx) with ctx = ctx0 + *ctx_dev; split-KV over
+ *         256-key chunks (work: fp32 [R][Hkv][max_splits][2G + G*hd], G <= 4).
+ * prefill: S queries per row at positions 0..S-1, causal (is_causal=S>1), V from v_rows.
+ * Output bf16 [rows][H*hd]. */
+int zk_attn_decode(const void* q, const void* k_cache, const void* vt_cache, int R, int H, int Hkv,
+                   int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int max_splits,
+                   void* out, const int32_t* skip, void* stream);
+int zk_attn_prefill(const void* q, const void* k_cache, const void* v_rows, int R, int S, int H,
+                    int Hkv, int hd, int Smax, void* out, void* stream);
+
+/* ------------------------------------------------------------------ graphs and timing
+ * The decode step is captured once into a hipGraph and replayed (the reference runs the
+ * transformer step eagerly: model.py:138-142, 220-222). */
+int zk_graph_begin(void* stream);
+int zk_graph_end(void* stream, void** graph_exec);
+int zk_graph_launch(void* graph_exec, int repeat, void* stream);
+int zk_graph_destroy(void* graph_exec);
+int zk_event_create(void** ev);
+int zk_event_record(void* ev, void* stream);
+int zk_event_elapsed_ms(void* start, void* end, float* ms);
+int zk_event_destroy(void* ev);
+
+/* ------------------------------------------------------------------ generation state machine
+ * One step of the generate() loop body after the backbone (model.py:353-424). */
+typedef struct zk_gen_state {
+    int32_t* scal;        /* device int32[16]: 0 offset, 1 pos, 2 step, 3 done, 4 any_new_eos,
+                             5 max_steps, 6 error flags */
+    int32_t* eos_mode;    /* [B] */
+    int32_t* steps_after; /* [B] */
+    int32_t* remaining;   /* [B] */
+    int32_t* stopping;    /* [B] */
+    int32_t* act;         /* [B] eos_active for the current step */
+    float* rp;            /* [B] repetition penalty in effect */
+    int32_t* tok0;        /* [B*K] draw-0 tokens */
+    int32_t* tok1;        /* [B*K] draw-1 (EOS resample) tokens */
+    int64_t* delayed;     /* [B][K][Ld] delayed codes (model.py:295) */
+    int32_t B, K, Ld, V;
+    uint64_t seed;
+    int32_t row_base;     /* global index of utterance 0 (batch sharding) */
+} zk_gen_state;
+
+/* Engine sampler: logits from the heads GEMM split-K slabs part [nsplit][2B][K*V] (rows
+ * [0,B) cond, [B,2B) uncond), bf16-rounded per head (model.py:111), CFG-combined
+ * (model.py:112-115), biased (model.py:322-324,353,360-362) and sampled. prefill=1 is the
+ * first sample (model.py:304: no bias, no penalty). draw 1 = EOS resample (model.py:386-393):
+ * a no-op unless some row has a new EOS. dbg_logits (nullable) receives the fp32 CFG logits
+ * before bias [B][K][V]. */
+int zk_sample_heads(const float* part, int nsplit, const zk_gen_state* st, const zk_sampling_params* sp,
+                    int prefill, int draw, float* dbg_logits, void* stream);
+/* EOS protocol + frame write + counters (model.py:376-424); prefill=1 only writes the
+ * first frame (model.py:310-319). */
+int zk_eos_step(const zk_gen_state* st, int prefill, int prefix_len, void* stream);
+
+/* ------------------------------------------------------------------ DAC decoder
+ * (zonos/autoencoder.py:44-47 -> modeling_dac.py:610-640). fp32 activations, layout
+ * [B][C][T] (channels-first, like torch). Per-row valid lengths (in frames) make a
+ * padded batch decode identical to per-utterance decode (autoencoder.py:219-226). */
+
+/* E_k[c][ch] = out_proj_k(codebook_k[c]) + bias_k  (modeling_dac.py:364-370), k < ncb. */
+int zk_dac_rvq_tables(const float* codebooks, const float* out_w, const float* out_b, int ncb,
+                      int ncode, int cdim, int hidden, float* tables, void* stream);
+/* z[b][ch][t] = sum_k E_k[codes[b][k][t]][ch] (sequential fp32, k ascending). */
+int zk_dac_rvq_decode(const int64_t* codes, int B, int ncb, int T, long code_bstride,
+                      const float* tables, int ncode, int hidden, float* z, int Tz,
+                      const int32_t* lens, void* stream);
+/* Generic conv over time with fused Snake input activation and epilogue:
+ *   out[b][co][t_out(q)] = bias[co] + sum_{ci,k} W[co][ci][k] * act(in[b][ci][q + k*dil - pad])
+ *                          (+ resid[b][co][t_out]) (tanh if do_tanh)
+ * t_out(q) = q*out_stride + out_off. act = Snake(alpha) if alpha != NULL (modeling_dac.py:95-100).
+ * in positions outside [0, len_in_b) read as 0; len_in_b = lens[b]*in_scale (lens NULL => Tin).
+ * Outputs outside [0, len_out_b) are written as 0. */
+int zk_dac_conv(const float* in, int B, int Cin, int Tin, const float* alpha,
+                const float* w, const float* bias, int Cout, int ks, int dil, int pad,
+                int Qn, int out_stride, int out_off, float* out, int Tout, const float* resid,
+                int do_tanh, const int32_t* lens, int in_scale, int out_scale, void* stream);
+/* ConvTranspose1d weight [Cin][Cout][2s] -> s polyphase 2-tap conv weights
+ * [s][Cout][Cin][2] so that zk_dac_conv(ks=2, pad=1, out_stride=s, out_off=r-ceil(s/2)). */
+int zk_dac_prep_convt(const float* w, int Cin, int Cout, int s, float* w_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZONOS_HIP_H */

@@ -1,0 +1,59 @@
+"""CPU: the C-ABI library builds/loads and exports every symbol include/zonos_hip.h declares;
+host-side logic that needs no GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "zonos_hip.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(zk_[a-z0-9_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from zonos_amd import build
+    path = build.build()
+    return ctypes.CDLL(path)
+
+
+def test_library_exports_header(lib):
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in zonos_hip.h but not exported"
+
+
+def test_python_binding_covers_header():
+    from zonos_amd import _lib
+    assert set(header_symbols()) == set(_lib.exported_symbols())
+
+
+def test_version_and_error_without_gpu(lib):
+    lib.zk_version.restype = ctypes.c_int
+    assert lib.zk_version() >= 1
+    lib.zk_last_error.restype = ctypes.c_char_p
+    assert isinstance(lib.zk_last_error(), bytes)
+
+
+def test_argument_validation_without_gpu(lib):
+    # shape checks run on the host before any launch
+    rc = lib.zk_gemm_bf16(None, ctypes.c_long(100), None, 0, 10, 64, 1, 0, None, None, None, None)
+    assert rc != 0
+    lib.zk_last_error.restype = ctypes.c_char_p
+    assert b"zk_gemm_bf16" in lib.zk_last_error()
+
+
+def test_split_selection_batch_invariant():
+    from zonos_amd.engine import _split_for
+    for N, K in ((3072, 2048), (2048, 2048), (2048, 8192), (9234, 2048)):
+        s = _split_for(N, K, 128)
+        assert K % (s * 64) == 0
+        assert all(_split_for(N, K, m) == s for m in (2, 8, 64, 128))
+        assert ((N + 63) // 64) * s >= 128

@@ -1,0 +1,223 @@
+"""GPU parity of the individual HIP kernels (through the C ABI) against the oracle /
+golden vectors. Tolerances are written next to each comparison."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import zonos_ref
+from oracle.philox import exp_noise
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from zonos_amd import _lib
+    _lib.load()
+
+
+def test_sampler_golden_exact():
+    """Sampled tokens == reference tokens (reference run with the same Philox noise)."""
+    from zonos_amd.sampling import sample_from_logits
+    d = np.load(os.path.join(G, "sampler.npz"))
+    mism = 0
+    total = 0
+    for ci in range(int(d["n_cases"])):
+        sp = {k[len(f"sp_{ci}_"):]: float(d[k]) for k in d.files if k.startswith(f"sp_{ci}_")}
+        sp["top_k"] = int(sp.get("top_k", 0))
+        sp["repetition_penalty_window"] = int(sp["repetition_penalty_window"])
+        sp.pop("repetition_penalty")
+        logits = torch.from_numpy(d[f"logits_{ci}"]).to(DEV)
+        tok = sample_from_logits(logits, generated_tokens=torch.from_numpy(d[f"gen_{ci}"].astype(np.int64)).to(DEV),
+                                 repetition_penalty=torch.from_numpy(d[f"rp_{ci}"]), seed=int(d["seed"]), step=ci + 1,
+                                 **sp)
+        got = tok.squeeze(-1).cpu().numpy()
+        exp = d[f"tok_{ci}"]
+        mism += int((got != exp).sum())
+        total += exp.size
+        if sp.get("temperature", 1.0) == 0:
+            assert np.array_equal(got, exp), f"greedy case {ci} must be bit-exact"
+    # sampled cases: fp32 softmax/exp differ in the last ulp between CPU and GPU; a flip needs
+    # an exact near-tie of probs/q. Allow at most 1 flipped token in all cases.
+    assert mism <= 1, f"{mism}/{total} sampled tokens differ"
+
+
+def test_noise_matches_oracle():
+    """Exponential-race noise stream: one-hot logits expose argmax(p/q) = argmin over ties of q."""
+    from zonos_amd.sampling import sample_from_logits
+    B, K, V = 3, 9, 1026
+    logits = torch.zeros(B, K, V, device=DEV)   # uniform probs -> token = argmin q
+    for step in (0, 5):
+        for draw in (0, 1):
+            tok = sample_from_logits(logits, temperature=1.0, repetition_penalty=1.0, seed=99, step=step, draw=draw,
+                                     row_base=7)
+            q = exp_noise(99, step, draw, B, K, V, row_base=7)
+            p = np.full((B, K, V), 1.0 / V, dtype=np.float32)
+            exp = np.argmax(p / q, axis=-1)
+            assert np.array_equal(tok.squeeze(-1).cpu().numpy(), exp)
+
+
+def test_delay_pattern_golden():
+    from zonos_amd.codebook_pattern import apply_delay_pattern, revert_delay_pattern
+    d = np.load(os.path.join(G, "delay.npz"))
+    codes = torch.from_numpy(d["codes"].astype(np.int64)).to(DEV)
+    dl = apply_delay_pattern(codes, 1025)
+    assert np.array_equal(dl.cpu().numpy(), d["delayed"])
+    assert np.array_equal(revert_delay_pattern(dl).cpu().numpy(), d["reverted"])
+    # empty time axis
+    e = apply_delay_pattern(torch.zeros(2, 9, 0, dtype=torch.int64, device=DEV), 1025)
+    assert e.shape == (2, 9, 9) and bool((e == 1025).all())
+
+
+@pytest.mark.parametrize("M,N,K,nsplit", [(128, 3072, 2048, 8), (7, 1026 * 9, 256, 2), (300, 192, 512, 1),
+                                          (128, 2048, 8192, 16)])
+def test_gemm_vs_fp32(M, N, K, nsplit):
+    from zonos_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    part = torch.empty(nsplit, M, N, device=DEV)
+    call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, nsplit, 0, ptr(part), None, None, stream_ptr())
+    got = part.sum(0)
+    ref = A.float() @ W.float().t()
+    # fp32 accumulation of bf16 products: error ~ K * eps32 * |a||w|
+    assert torch.allclose(got, ref, atol=2e-3 * (K / 2048) ** 0.5, rtol=1e-3), (got - ref).abs().max()
+
+
+def test_gemm_swiglu():
+    from zonos_amd._lib import call, ptr, stream_ptr
+    M, Fd, D = 130, 256, 512
+    g = torch.Generator(device="cpu").manual_seed(1)
+    A = torch.randn(M, D, generator=g).to(torch.bfloat16)
+    W1 = (torch.randn(2 * Fd, D, generator=g) / D ** 0.5).to(torch.bfloat16)
+    ref_y, ref_g = F.linear(A, W1).chunk(2, dim=-1)      # bf16 CPU like the reference
+    ref = ref_y * F.silu(ref_g)
+    Wp = torch.empty_like(W1).to(DEV)
+    s = stream_ptr()
+    call("zk_permute_fc1", ptr(W1.to(DEV)), Fd, D, ptr(Wp), s)
+    A_d = A.to(DEV)
+    out = torch.empty(M, Fd, dtype=torch.bfloat16, device=DEV)
+    call("zk_gemm_bf16", ptr(A_d), D, ptr(Wp), M, 2 * Fd, D, 1, 1, None, ptr(out), None, s)
+    err = (out.float().cpu() - ref.float()).abs()
+    # one bf16 ulp of the product (|h| < 4 here) plus accumulation-order flips of y/gate
+    assert err.max() < 0.05 and (err > 0).float().mean() < 0.05, err.max()
+
+
+def test_layernorm_and_resid_ln():
+    from zonos_amd._lib import call, ptr, stream_ptr
+    for D in (256, 2048):
+        rows = 33
+        g = torch.Generator(device="cpu").manual_seed(D)
+        x = torch.randn(rows, D, generator=g).to(torch.bfloat16)
+        w = (1 + 0.1 * torch.randn(D, generator=g)).to(torch.bfloat16)
+        b = (0.1 * torch.randn(D, generator=g)).to(torch.bfloat16)
+        part = torch.randn(3, rows, D, generator=g)
+        ref_ln = F.layer_norm(x, (D,), w, b, 1e-5)
+        y = torch.empty(rows, D, dtype=torch.bfloat16, device=DEV)
+        xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+        s = stream_ptr()
+        call("zk_layernorm", ptr(xd), ptr(wd), ptr(bd), 1e-5, rows, D, ptr(y), s)
+        assert (y.float().cpu() - ref_ln.float()).abs().max() < 0.04   # ~1 bf16 ulp at |y|<5
+        ref_x = x + part.sum(0).to(torch.bfloat16)
+        ref_xn = F.layer_norm(ref_x, (D,), w, b, 1e-5)
+        xo = torch.empty_like(xd)
+        xn = torch.empty_like(xd)
+        pd = part.to(DEV)
+        call("zk_resid_ln", ptr(pd), 3, ptr(xd), ptr(wd), ptr(bd), 1e-5, rows, D, ptr(xo), ptr(xn), None, s)
+        assert (xo.float().cpu() - ref_x.float()).abs().max() < 0.07
+        assert (xn.float().cpu() - ref_xn.float()).abs().max() < 0.06
+
+
+def _attn_setup(R, S_ctx, H, Hk, hd, smax, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    k = torch.randn(R, S_ctx, Hk, hd, generator=g).to(torch.bfloat16)
+    v = torch.randn(R, S_ctx, Hk, hd, generator=g).to(torch.bfloat16)
+    kc = torch.zeros(R, Hk, smax, hd, dtype=torch.bfloat16)
+    vt = torch.zeros(R, Hk, hd, smax, dtype=torch.bfloat16)
+    kc[:, :, :S_ctx] = k.transpose(1, 2)
+    vt[:, :, :, :S_ctx] = v.permute(0, 2, 3, 1)
+    return k, v, kc, vt
+
+
+@pytest.mark.parametrize("R,ctx,H,Hk", [(4, 1, 16, 4), (3, 300, 16, 4), (2, 1000, 2, 1), (128, 513, 16, 4)])
+def test_attention_decode(R, ctx, H, Hk):
+    from zonos_amd._lib import call, ptr, stream_ptr
+    hd = 128
+    smax = ((ctx + 255) // 256) * 256
+    k, v, kc, vt = _attn_setup(R, ctx, H, Hk, hd, smax)
+    q = torch.randn(R, 1, H, hd).to(torch.bfloat16)
+    ref = F.scaled_dot_product_attention(q.transpose(1, 2).float(), k.transpose(1, 2).float(),
+                                         v.transpose(1, 2).float(), enable_gqa=True).transpose(1, 2).reshape(R, H * hd)
+    max_splits = smax // 256
+    work = torch.empty(R * Hk * max_splits * (8 + 4 * hd), device=DEV)
+    out = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
+    qd, kd, vd = q.to(DEV), kc.to(DEV), vt.to(DEV)
+    call("zk_attn_decode", ptr(qd), ptr(kd), ptr(vd), R, H, Hk, hd, smax, ctx, None, ptr(work), max_splits, ptr(out),
+         None, stream_ptr())
+    # P is rounded to bf16 for the P.V MFMA (as the reference's CPU flash kernel does)
+    assert (out.float().cpu() - ref).abs().max() < 2e-2
+
+
+@pytest.mark.parametrize("R,S,H,Hk", [(2, 1, 2, 1), (3, 70, 16, 4), (2, 200, 2, 1)])
+def test_attention_prefill(R, S, H, Hk):
+    from zonos_amd._lib import call, ptr, stream_ptr
+    hd = 128
+    smax = ((S + 255) // 256) * 256
+    k, v, kc, vt = _attn_setup(R, S, H, Hk, hd, smax, seed=3)
+    q = torch.randn(R, S, H, hd).to(torch.bfloat16)
+    ref = F.scaled_dot_product_attention(q.transpose(1, 2).float(), k.transpose(1, 2).float(),
+                                         v.transpose(1, 2).float(), is_causal=S > 1, enable_gqa=True)
+    ref = ref.transpose(1, 2).reshape(R * S, H * hd)
+    vrows = v.permute(0, 2, 1, 3).contiguous().to(DEV)     # [R][Hkv][S][hd]
+    out = torch.empty(R * S, H * hd, dtype=torch.bfloat16, device=DEV)
+    qd, kd = q.reshape(R * S, H * hd).to(DEV), kc.to(DEV)
+    call("zk_attn_prefill", ptr(qd), ptr(kd), ptr(vrows), R, S, H, Hk, hd, smax, ptr(out), stream_ptr())
+    assert (out.float().cpu() - ref).abs().max() < 1e-2
+
+
+def test_qkv_rope_matches_oracle():
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import rope_table
+    R, S, H, Hk, hd, smax = 2, 5, 2, 1, 128, 256
+    N = (H + 2 * Hk) * hd
+    g = torch.Generator(device="cpu").manual_seed(7)
+    part = torch.randn(2, R * S, N, generator=g)
+    qkv = part.sum(0).to(torch.bfloat16).view(R, S, N)
+    fr = rope_table(16384, hd)
+    pos0 = 11
+    fc = fr[torch.arange(S)[None, :] + pos0].expand(R, -1, -1, -1)
+    qr, kr, vr = qkv.split([H * hd, Hk * hd, Hk * hd], dim=-1)
+    q_ref = zonos_ref.rope(qr.reshape(R, S, H, hd), fc).reshape(R * S, H * hd)
+    k_ref = zonos_ref.rope(kr.reshape(R, S, Hk, hd), fc)
+    q = torch.empty(R * S, H * hd, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(R, Hk, smax, hd, dtype=torch.bfloat16, device=DEV)
+    vt = torch.zeros(R, Hk, hd, smax, dtype=torch.bfloat16, device=DEV)
+    vrows = torch.zeros(R, Hk, S, hd, dtype=torch.bfloat16, device=DEV)
+    pd, fd = part.to(DEV), fr.to(DEV)
+    call("zk_qkv_rope", ptr(pd), 2, R, S, H, Hk, hd, ptr(fd), pos0, None, ptr(q), ptr(kc), ptr(vt), smax, ptr(vrows),
+         None, stream_ptr())
+    # slab sums in a different order can flip one bf16 rounding; then RoPE is exact fp32
+    assert (q.float().cpu() - q_ref.float()).abs().max() < 0.05
+    assert (kc[:, :, pos0:pos0 + S].transpose(1, 2).float().cpu() - k_ref.float()).abs().max() < 0.05
+    assert torch.equal(vt[:, :, :, pos0:pos0 + S].permute(0, 3, 1, 2).cpu(), vr.reshape(R, S, Hk, hd))
+    assert torch.equal(vrows.permute(0, 2, 1, 3).cpu(), vr.reshape(R, S, Hk, hd))
+
+
+def test_embed_codes():
+    from zonos_amd._lib import call, ptr, stream_ptr
+    B, S, K, V, D = 3, 4, 9, 1026, 256
+    g = torch.Generator(device="cpu").manual_seed(2)
+    emb = torch.randn(K, V, D, generator=g).to(torch.bfloat16)
+    ids = torch.randint(0, V, (B, K, S), generator=g)
+    W = {f"embeddings.{k}.weight": emb[k] for k in range(K)}
+    ref = zonos_ref.embed_codes(W, zonos_ref.BackboneCfg(d_model=D), ids).repeat(2, 1, 1)
+    out = torch.zeros(2 * B, S + 2, D, dtype=torch.bfloat16, device=DEV)
+    idd, ed = ids.to(DEV), emb.to(DEV)
+    call("zk_embed_codes", ptr(idd), B, S, K, K * S, S, None, 0, ptr(ed), V, D, 2, ptr(out), S + 2, 2, None, None,
+         1e-5, None, None, stream_ptr())
+    assert torch.equal(out[:, 2:].cpu(), ref)          # bf16 sequential adds reproduced bit-exactly

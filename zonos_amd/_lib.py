@@ -1,0 +1,120 @@
+"""ctypes binding of libzonos_hip.so (the C ABI declared in include/zonos_hip.h).
+
+The product path has no fallback: if the library is missing or fails to load, every
+entry point raises. Device buffers are torch tensors; only their data_ptr() crosses the
+ABI together with plain ints/floats and the current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes as C  # noqa: N812
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libzonos_hip.so")
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_long
+F = C.c_float
+U64 = C.c_uint64
+I64 = C.c_int64
+
+
+class SamplingParams(C.Structure):
+    _fields_ = [("temperature", F), ("top_p", F), ("min_p", F), ("linear", F), ("conf", F), ("quad", F),
+                ("top_k", C.c_int32), ("rp_window", C.c_int32), ("cfg_scale", F),
+                ("force_full_length", C.c_int32)]
+
+
+class GenState(C.Structure):
+    _fields_ = [("scal", P), ("eos_mode", P), ("steps_after", P), ("remaining", P), ("stopping", P),
+                ("act", P), ("rp", P), ("tok0", P), ("tok1", P), ("delayed", P),
+                ("B", C.c_int32), ("K", C.c_int32), ("Ld", C.c_int32), ("V", C.c_int32),
+                ("seed", U64), ("row_base", C.c_int32)]
+
+
+# name -> argtypes (all return int status)
+_SIGS = {
+    "zk_version": [],
+    "zk_device_sync": [],
+    "zk_sample_logits": [P, I, I, I, P, I, I, P, C.POINTER(SamplingParams), U64, I, I, I, P, P],
+    "zk_delay_apply": [P, I, I, I, I64, P, P],
+    "zk_delay_revert": [P, I, I, I, P, P],
+    "zk_embed_codes": [P, I, I, I, L, L, P, I, P, I, I, I, P, I, I, P, P, F, P, P, P],
+    "zk_layernorm": [P, P, P, F, I, I, P, P],
+    "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, P, P],
+    "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
+    "zk_permute_fc1": [P, I, I, P, P],
+    "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, P, P],
+    "zk_attn_decode": [P, P, P, I, I, I, I, I, I, P, P, I, P, P, P],
+    "zk_attn_prefill": [P, P, P, I, I, I, I, I, I, P, P],
+    "zk_sample_heads": [P, I, C.POINTER(GenState), C.POINTER(SamplingParams), I, I, P, P],
+    "zk_eos_step": [C.POINTER(GenState), I, I, P],
+    "zk_graph_begin": [P],
+    "zk_graph_end": [P, C.POINTER(P)],
+    "zk_graph_launch": [P, I, P],
+    "zk_graph_destroy": [P],
+    "zk_event_create": [C.POINTER(P)],
+    "zk_event_record": [P, P],
+    "zk_event_elapsed_ms": [P, P, C.POINTER(F)],
+    "zk_event_destroy": [P],
+    "zk_dac_rvq_tables": [P, P, P, I, I, I, I, P, P],
+    "zk_dac_rvq_decode": [P, I, I, I, L, P, I, I, P, I, P, P],
+    "zk_dac_conv": [P, I, I, I, P, P, P, I, I, I, I, I, I, I, P, I, P, I, P, I, I, P],
+    "zk_dac_prep_convt": [P, I, I, I, P, P],
+}
+
+_lib = None
+
+
+class ZonosHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (and type) the library. Raises ZonosHipError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ZonosHipError(f"{LIB_PATH} not found: build it with `python -m zonos_amd.build` "
+                            "(there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    lib.zk_last_error.restype = C.c_char_p
+    lib.zk_last_error.argtypes = []
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGS) + ["zk_last_error"]
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise ZonosHipError(f"{name} failed ({rc}): {lib.zk_last_error().decode()}")
+    return rc
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(t: torch.Tensor, name: str = "tensor"):
+    if not t.is_cuda:
+        raise ZonosHipError(f"{name} must be a GPU tensor (the HIP engine has no CPU path)")

@@ -1,0 +1,308 @@
+"""DAC decoder on the GPU: the decode half of zonos/autoencoder.py (DACAutoencoder.decode
+44-47, codes_to_wavs 188-245, save_codes 247-268) over hand-written HIP kernels
+(zonos_amd/csrc/dac.hip), restating transformers' DacModel.decode (modeling_dac.py:610-640).
+
+Batching: codes_to_wavs in the reference decodes one utterance at a time
+(autoencoder.py:219-226). Here a list of utterances is decoded as ONE zero-padded batch
+with per-row valid lengths; every conv reads zeros beyond a row's length, which is
+exactly the padding the standalone decode of that row would see, so each waveform equals
+its per-utterance decode.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+
+class DacSpec:
+    """descript/dac_44khz decoder geometry (configuration_dac.py defaults)."""
+
+    def __init__(self, hidden_size=1024, decoder_hidden_size=1536, upsampling_ratios=(8, 8, 4, 2), n_codebooks=9,
+                 codebook_size=1024, codebook_dim=8, sampling_rate=44100):
+        self.hidden_size = hidden_size
+        self.decoder_hidden_size = decoder_hidden_size
+        self.upsampling_ratios = tuple(upsampling_ratios)
+        self.n_codebooks = n_codebooks
+        self.codebook_size = codebook_size
+        self.codebook_dim = codebook_dim
+        self.sampling_rate = sampling_rate
+
+    @property
+    def hop_length(self):
+        return int(math.prod(self.upsampling_ratios))
+
+    @classmethod
+    def from_hf_config(cls, d: dict) -> "DacSpec":
+        return cls(d.get("hidden_size", 1024), d.get("decoder_hidden_size", 1536),
+                   tuple(d.get("upsampling_ratios", (8, 8, 4, 2))), d.get("n_codebooks", 9),
+                   d.get("codebook_size", 1024), d.get("codebook_dim", 8), d.get("sampling_rate", 44100))
+
+
+def _fold_weight_norm(sd: dict) -> dict:
+    """Accept weight-normalised checkpoints (weight_g/weight_v or parametrizations.*.original0/1)."""
+    out = dict(sd)
+    for k in list(sd):
+        for g_suf, v_suf, base in ((".weight_g", ".weight_v", ".weight"),
+                                   (".parametrizations.weight.original0", ".parametrizations.weight.original1",
+                                    ".weight")):
+            if k.endswith(g_suf):
+                stem = k[: -len(g_suf)]
+                g, v = sd[k].float(), sd[stem + v_suf].float()
+                norm = v.flatten(1).norm(dim=1).view(-1, *([1] * (v.dim() - 1)))
+                out[stem + base] = g * v / norm
+                out.pop(k, None)
+                out.pop(stem + v_suf, None)
+    return out
+
+
+class HipDacDecoder:
+    """Decoder weights on the device (fp32) + the launch sequence of the DAC decoder."""
+
+    def __init__(self, spec: DacSpec, state_dict: dict, device="cuda"):
+        _lib.load()
+        self.spec = spec
+        self.device = torch.device(device)
+        sd = _fold_weight_norm(state_dict)
+        dev = self.device
+
+        def t(k):
+            return sd[k].to(device=dev, dtype=torch.float32).contiguous()
+
+        s = spec
+        stream = _lib.stream_ptr(dev)
+        cbs = torch.stack([t(f"quantizer.quantizers.{k}.codebook.weight") for k in range(s.n_codebooks)])
+        ows = torch.stack([t(f"quantizer.quantizers.{k}.out_proj.weight").reshape(s.hidden_size, s.codebook_dim)
+                           for k in range(s.n_codebooks)])
+        obs = torch.stack([t(f"quantizer.quantizers.{k}.out_proj.bias") for k in range(s.n_codebooks)])
+        self.tables = torch.empty(s.n_codebooks, s.codebook_size, s.hidden_size, device=dev)
+        call("zk_dac_rvq_tables", ptr(cbs.contiguous()), ptr(ows.contiguous()), ptr(obs.contiguous()),
+             s.n_codebooks, s.codebook_size, s.codebook_dim, s.hidden_size, ptr(self.tables), stream)
+        self.conv1_w, self.conv1_b = t("decoder.conv1.weight"), t("decoder.conv1.bias")
+        self.blocks = []
+        for i, st in enumerate(s.upsampling_ratios):
+            p = f"decoder.block.{i}."
+            wt = t(p + "conv_t1.weight")                      # [Cin][Cout][2s]
+            cin, cout = wt.shape[0], wt.shape[1]
+            wprep = torch.empty(st, cout, cin, 2, device=dev)
+            call("zk_dac_prep_convt", ptr(wt), cin, cout, st, ptr(wprep), stream)
+            blk = dict(stride=st, cin=cin, cout=cout, alpha=t(p + "snake1.alpha").reshape(-1), wt=wprep,
+                       bt=t(p + "conv_t1.bias"), res=[])
+            for r, dil in ((1, 1), (2, 3), (3, 9)):
+                u = p + f"res_unit{r}."
+                blk["res"].append(dict(dil=dil, a1=t(u + "snake1.alpha").reshape(-1), w1=t(u + "conv1.weight"),
+                                       b1=t(u + "conv1.bias"), a2=t(u + "snake2.alpha").reshape(-1),
+                                       w2=t(u + "conv2.weight"), b2=t(u + "conv2.bias")))
+            self.blocks.append(blk)
+        self.final_alpha = t("decoder.snake1.alpha").reshape(-1)
+        self.conv2_w, self.conv2_b = t("decoder.conv2.weight"), t("decoder.conv2.bias")
+        torch.cuda.synchronize(dev)
+
+    def _conv(self, x, B, Cin, Tin, alpha, w, b, Cout, ks, dil, pad, Qn, ostride, ooff, out, Tout, resid, tanh,
+              lens, in_scale, out_scale, stream):
+        call("zk_dac_conv", ptr(x), B, Cin, Tin, ptr(alpha), ptr(w), ptr(b), Cout, ks, dil, pad, Qn, ostride, ooff,
+             ptr(out), Tout, ptr(resid), int(tanh), ptr(lens), in_scale, out_scale, stream)
+
+    @torch.inference_mode()
+    def decode_padded(self, codes: torch.Tensor, lens: torch.Tensor | None = None) -> torch.Tensor:
+        """codes int64 [B][9][T] on device -> waveform fp32 [B][1][hop*T].
+        lens (int32 [B], frames) marks each row's valid length; None = all T."""
+        s = self.spec
+        dev = self.device
+        codes = codes.to(device=dev, dtype=torch.int64).contiguous()
+        B, K, T = codes.shape
+        assert K == s.n_codebooks, f"Expected {s.n_codebooks} codebooks, got {K}"   # autoencoder.py:45
+        stream = _lib.stream_ptr(dev)
+        if lens is not None:
+            lens = lens.to(device=dev, dtype=torch.int32).contiguous()
+        z = torch.empty(B, s.hidden_size, T, device=dev)
+        call("zk_dac_rvq_decode", ptr(codes), B, K, T, K * T, ptr(self.tables), s.codebook_size, s.hidden_size,
+             ptr(z), T, ptr(lens), stream)
+        C0 = self.conv1_w.shape[0]
+        x = torch.empty(B, C0, T, device=dev)
+        self._conv(z, B, s.hidden_size, T, None, self.conv1_w, self.conv1_b, C0, 7, 1, 3, T, 1, 0, x, T, None,
+                   False, lens, 1, 1, stream)
+        del z
+        L, scale = T, 1
+        for blk in self.blocks:
+            st, cin, cout = blk["stride"], blk["cin"], blk["cout"]
+            Lo = L * st
+            y = torch.empty(B, cout, Lo, device=dev)
+            p = math.ceil(st / 2)
+            for r in range(st):
+                self._conv(x, B, cin, L, blk["alpha"], blk["wt"][r], blk["bt"], cout, 2, 1, 1, L + 1, st, r - p, y,
+                           Lo, None, False, lens, scale, scale * st, stream)
+            del x
+            scale *= st
+            L = Lo
+            tmp = torch.empty_like(y)
+            for ru in blk["res"]:
+                d = ru["dil"]
+                self._conv(y, B, cout, L, ru["a1"], ru["w1"], ru["b1"], cout, 7, d, 3 * d, L, 1, 0, tmp, L, None,
+                           False, lens, scale, scale, stream)
+                self._conv(tmp, B, cout, L, ru["a2"], ru["w2"], ru["b2"], cout, 1, 1, 0, L, 1, 0, y, L, y, False,
+                           lens, scale, scale, stream)
+            del tmp
+            x = y
+        out = torch.empty(B, 1, L, device=dev)
+        cl = x.shape[1]
+        self._conv(x, B, cl, L, self.final_alpha, self.conv2_w, self.conv2_b, 1, 7, 1, 3, L, 1, 0, out, L, None,
+                   True, lens, scale, scale, stream)
+        return out
+
+    def decode_list(self, codes_list, max_batch_elems: float = 6e9) -> list:
+        """Per-utterance waveforms for a list of [9, T_i] / [1, 9, T_i] code tensors, decoded as
+        zero-padded batches (chunks bounded by activation memory)."""
+        items = []
+        for c in codes_list:
+            c = c.unsqueeze(0) if c.dim() == 2 else c
+            for j in range(c.shape[0]):
+                items.append(c[j])
+        results = [None] * len(items)
+        order = [i for i in range(len(items)) if items[i].shape[1] > 0]
+        order.sort(key=lambda i: -items[i].shape[1])
+        hop = self.spec.hop_length
+        width = self.blocks[-1]["cout"] if self.blocks else self.spec.decoder_hidden_size
+        i = 0
+        while i < len(order):
+            Tmax = items[order[i]].shape[1]
+            per = max(1, int(max_batch_elems // (3 * width * hop * Tmax)))
+            grp = order[i:i + per]
+            codes = torch.zeros(len(grp), self.spec.n_codebooks, Tmax, dtype=torch.int64, device=self.device)
+            lens = torch.tensor([items[g].shape[1] for g in grp], dtype=torch.int32)
+            for j, g in enumerate(grp):
+                codes[j, :, :items[g].shape[1]] = items[g].to(self.device)
+            wav = self.decode_padded(codes, lens)
+            for j, g in enumerate(grp):
+                results[g] = wav[j, :, : int(lens[j]) * hop]
+            i += per
+        return [r for r in results if r is not None]
+
+
+class DACAutoencoder:
+    """API mirror of zonos/autoencoder.py:12-268 (decode side).
+
+    Weights: ``DACAutoencoder(state_dict=...)``, ``DACAutoencoder.from_local(dir_or_file)``
+    (a HF-format DacModel safetensors), or the local HF cache of "descript/dac_44khz"
+    (autoencoder.py:15 fetches it by name; offline only the cache is consulted)."""
+
+    def __init__(self, state_dict: dict | None = None, spec: DacSpec | None = None, device="cuda"):
+        self.spec = spec or DacSpec()
+        if state_dict is None:
+            state_dict, cfg = _load_hf_cache("descript/dac_44khz")
+            if cfg is not None:
+                self.spec = DacSpec.from_hf_config(cfg)
+        self.decoder = HipDacDecoder(self.spec, state_dict, device)
+        self.codebook_size = self.spec.codebook_size
+        self.num_codebooks = self.spec.n_codebooks
+        self.sampling_rate = self.spec.sampling_rate
+
+    @classmethod
+    def from_local(cls, path: str, device="cuda") -> "DACAutoencoder":
+        sd, cfg = _load_safetensors_dir(path)
+        return cls(sd, DacSpec.from_hf_config(cfg) if cfg else None, device)
+
+    def decode(self, codes: torch.Tensor) -> torch.Tensor:
+        """autoencoder.py:44-47: [B, 9, T] -> fp32 [B, 1, 512*T] (all rows full length)."""
+        assert codes.shape[1] == self.num_codebooks, \
+            f"Expected {self.num_codebooks} codebooks, got {codes.shape[1]}"
+        return self.decoder.decode_padded(codes)
+
+    def decode_list(self, codes) -> list:
+        return self.decoder.decode_list(codes)
+
+    # ---- post-processing of codes_to_wavs (autoencoder.py:49-90, 172-245) -- host side, per file
+    @staticmethod
+    def trim_silence(wav: torch.Tensor, threshold: float = 1e-5, frame_size: int = 512) -> torch.Tensor:
+        n = min((wav.shape[1] // frame_size) // 4, 16)
+        start, end = 0, wav.shape[1]
+        for i in range(n):
+            if wav[:, i * frame_size:(i + 1) * frame_size].pow(2).mean() > threshold:
+                start = i * frame_size
+                break
+        for i in range(n):
+            fr = wav[:, -((i + 1) * frame_size): -i * frame_size] if i else wav[:, -frame_size:]
+            if fr.pow(2).mean() > threshold:
+                end = wav.shape[1] - (i + 1) * frame_size
+                break
+        return wav[:, start:end] if (start > 0 or end < wav.shape[1]) else wav
+
+    def normalize_loudness(self, audio, sr, target_lufs=-19.0):
+        try:
+            import pyloudnorm
+            block = 0.400 if audio.shape[1] > 2.0 * sr else 0.100
+            loud = pyloudnorm.Meter(sr, block_size=block).integrated_loudness(audio.cpu().numpy().T)
+            return audio * (10 ** ((target_lufs - loud) / 20.0))
+        except Exception:
+            return audio
+
+    def codes_to_wavs(self, codes) -> list:
+        if isinstance(codes, torch.Tensor):
+            if codes.dim() == 2:
+                codes = [codes]
+            elif codes.dim() == 3:
+                codes = [codes[i] for i in range(codes.shape[0])]
+            else:
+                raise ValueError(f"Invalid shape for codes: {codes.shape}")
+        wavs = self.decode_list(codes)
+        out = []
+        for wav in wavs:
+            wav = wav.cpu()
+            wav = self.normalize_loudness(wav, self.sampling_rate, -23.0)
+            wav = self.trim_silence(wav)
+            bs = 512
+            wav[:, :bs] *= torch.linspace(0, 1, min(bs, wav.shape[1])).unsqueeze(0)[:, :wav[:, :bs].shape[1]]
+            nb = min((wav.shape[1] // bs) // 4, 20)
+            if nb > 0:
+                wav[:, -(nb * bs):] *= torch.logspace(0, -10, nb * bs).unsqueeze(0)
+            out.append(wav)
+        return out
+
+    def save_codes(self, paths, codes) -> None:
+        if isinstance(paths, str):
+            paths = [paths]
+        wavs = self.codes_to_wavs(codes)
+        assert len(paths) == len(wavs), f"Number of paths ({len(paths)}) must match number of codes ({len(wavs)})"
+        import wave
+
+        import numpy as np
+        for p, w in zip(paths, wavs):
+            pcm = (w.clamp(-1, 1).squeeze(0).numpy() * 32767.0).astype(np.int16)
+            with wave.open(p, "wb") as f:
+                f.setnchannels(1)
+                f.setsampwidth(2)
+                f.setframerate(self.sampling_rate)
+                f.writeframes(pcm.tobytes())
+
+
+def _load_safetensors_dir(path: str):
+    import json
+
+    from safetensors.torch import load_file
+    cfg = None
+    if os.path.isdir(path):
+        cj = os.path.join(path, "config.json")
+        if os.path.exists(cj):
+            cfg = json.load(open(cj))
+        files = [os.path.join(path, f) for f in os.listdir(path) if f.endswith(".safetensors")]
+    else:
+        files = [path]
+    sd = {}
+    for f in files:
+        sd.update(load_file(f))
+    return sd, cfg
+
+
+def _load_hf_cache(repo_id: str):
+    from huggingface_hub import snapshot_download
+    try:
+        d = snapshot_download(repo_id, local_files_only=True)
+    except Exception as e:   # no network in this environment
+        raise FileNotFoundError(
+            f"{repo_id} is not in the local Hugging Face cache; pass state_dict= or use "
+            f"DACAutoencoder.from_local(path)") from e
+    return _load_safetensors_dir(d)

@@ -1,0 +1,494 @@
+// Transformer backbone step kernels for gfx950 (zonos/backbone/_torch.py restated).
+//
+//   k_embed_ln   : sum of 9 codebook embeddings (bf16 left-to-right adds, model.py:97-98),
+//                  duplicated for the CFG rows (model.py:141) + layer-0 LayerNorm.
+//   k_resid_ln   : split-K slab reduction of the preceding projection + residual add
+//                  (bf16, _torch.py:100-101) + the next LayerNorm, one pass over the row.
+//   k_qkv_rope   : in_proj slab reduction -> bf16 -> interleaved RoPE (_torch.py:18-30)
+//                  -> q buffer + KV cache store (_torch.py:33-49).
+//   k_attn_decode: split-KV GQA decode attention on MFMA 16x16x32 bf16 (K on the A side,
+//                  the 4 query heads of a KV head on the B side), k_attn_combine merges splits.
+//   k_attn_prefill: causal prefill attention, one wave per query, 64-key chunks.
+//
+// KV cache layout (engine-owned, not the reference's [R,S,2,Hkv,hd]):
+//   K   [R][Hkv][Smax][hd]   -- a key row is 256 contiguous bytes (A-operand loads)
+//   V^T [R][Hkv][hd][Smax]   -- 8 consecutive keys of one channel are contiguous
+//                               (B-operand loads of P.V)
+#include "common.h"
+#include "../../include/zonos_hip.h"
+#include <algorithm>
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+ZK_DEV bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// ------------------------------------------------------------------ LayerNorm helper
+// Row of D elements, 8 per thread (D = 8 * NT * n8). Two-pass mean/var in fp32,
+// y = (x - mean) * rstd * w + b rounded to bf16 (nn.LayerNorm, eps from config).
+template <int NT, int n8>
+ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, int D, bf16_t* y,
+                   float* red) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < n8; ++j)
+        if ((threadIdx.x + NT * j) * 8 < D)
+            for (int e = 0; e < 8; ++e) s += x[j * 8 + e];
+    const float mean = block_sum<NT>(s, red) / (float)D;
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < n8; ++j)
+        if ((threadIdx.x + NT * j) * 8 < D)
+            for (int e = 0; e < 8; ++e) { const float d = x[j * 8 + e] - mean; v += d * d; }
+    const float var = block_sum<NT>(v, red) / (float)D;
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int j = 0; j < n8; ++j) {
+        const int c = (threadIdx.x + NT * j) * 8;
+        if (c >= D) continue;
+        float wf[8], bf[8], o[8];
+        unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
+        unpack8(*reinterpret_cast<const uint4*>(b + c), bf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (x[j * 8 + e] - mean) * rstd * wf[e] + bf[e];
+        *reinterpret_cast<uint4*>(y + c) = pack8(o);
+    }
+}
+
+constexpr int LN_NT = 256;
+constexpr int MAX_N8 = 4;     // D <= 8192
+
+template <int N8>
+__global__ __launch_bounds__(LN_NT) void k_embed_ln(const int64_t* ids, int B, int S, int K, long bstr, long kstr,
+                                                    const int32_t* col_dev, int col_add, const bf16_t* emb, int V,
+                                                    int D, bf16_t* x_out, int out_S, int out_t0, const bf16_t* lw,
+                                                    const bf16_t* lb, float eps, bf16_t* xn_out, const int32_t* skip) {
+    __shared__ float red[LN_NT / 64];
+    if (skip && *skip) return;
+    const int r = blockIdx.x / S, t = blockIdx.x % S, b = r % B;
+    const int row = r * out_S + out_t0 + t;   // output row
+    const int col = t + (col_dev ? *col_dev + col_add : 0);
+    constexpr int n8 = N8;
+    float x[N8 * 8];
+#pragma unroll
+    for (int j = 0; j < n8; ++j) {
+        const int c = (threadIdx.x + LN_NT * j) * 8;
+        if (c >= D) continue;
+        float acc[8];
+        for (int k = 0; k < K; ++k) {
+            int64_t id = ids[b * bstr + k * kstr + col];
+            id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+            float e[8];
+            unpack8(*reinterpret_cast<const uint4*>(emb + ((size_t)k * V + id) * D + c), e);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] = (k == 0) ? e[q] : round_bf(acc[q] + e[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[j * 8 + q] = acc[q];
+        *reinterpret_cast<uint4*>(x_out + (size_t)row * D + c) = pack8(acc);
+    }
+    if (lw != nullptr) ln_row<LN_NT, N8>(x, lw, lb, eps, D, xn_out + (size_t)row * D, red);
+}
+
+template <int N8>
+__global__ __launch_bounds__(LN_NT) void k_layernorm(const bf16_t* x, const bf16_t* w, const bf16_t* b, float eps,
+                                                     int D, bf16_t* y) {
+    __shared__ float red[LN_NT / 64];
+    const int row = blockIdx.x;
+    constexpr int n8 = N8;
+    float xv[N8 * 8];
+#pragma unroll
+    for (int j = 0; j < n8; ++j) {
+        const int c = (threadIdx.x + LN_NT * j) * 8;
+        if (c >= D) continue;
+        unpack8(*reinterpret_cast<const uint4*>(x + (size_t)row * D + c), xv + 8 * j);
+    }
+    ln_row<LN_NT, N8>(xv, w, b, eps, D, y + (size_t)row * D, red);
+}
+
+template <int N8>
+__global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nsplit, const bf16_t* x_in,
+                                                    const bf16_t* w, const bf16_t* b, float eps, int rows, int D,
+                                                    bf16_t* x_out, bf16_t* xn_out, const int32_t* skip) {
+    __shared__ float red[LN_NT / 64];
+    if (skip && *skip) return;
+    const int row = blockIdx.x;
+    constexpr int n8 = N8;
+    const size_t slab = (size_t)rows * D;
+    float xv[N8 * 8];
+#pragma unroll
+    for (int j = 0; j < n8; ++j) {
+        const int c = (threadIdx.x + LN_NT * j) * 8;
+        if (c >= D) continue;
+        const float* p = part + (size_t)row * D + c;
+        float acc[8];
+        {
+            const float4 a0 = *reinterpret_cast<const float4*>(p);
+            const float4 a1 = *reinterpret_cast<const float4*>(p + 4);
+            acc[0] = a0.x; acc[1] = a0.y; acc[2] = a0.z; acc[3] = a0.w;
+            acc[4] = a1.x; acc[5] = a1.y; acc[6] = a1.z; acc[7] = a1.w;
+        }
+        for (int s = 1; s < nsplit; ++s) {
+            const float4 a0 = *reinterpret_cast<const float4*>(p + s * slab);
+            const float4 a1 = *reinterpret_cast<const float4*>(p + s * slab + 4);
+            acc[0] += a0.x; acc[1] += a0.y; acc[2] += a0.z; acc[3] += a0.w;
+            acc[4] += a1.x; acc[5] += a1.y; acc[6] += a1.z; acc[7] += a1.w;
+        }
+        float xi[8];
+        unpack8(*reinterpret_cast<const uint4*>(x_in + (size_t)row * D + c), xi);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[j * 8 + e] = round_bf(xi[e] + round_bf(acc[e]));
+        *reinterpret_cast<uint4*>(x_out + (size_t)row * D + c) = pack8(xv + 8 * j);
+    }
+    ln_row<LN_NT, N8>(xv, w, b, eps, D, xn_out + (size_t)row * D, red);
+}
+
+// ------------------------------------------------------------------ in_proj epilogue
+__global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv,
+                                                  int hd, const float* freqs, int pos0, const int32_t* pos_dev,
+                                                  bf16_t* q_out, bf16_t* kc, bf16_t* vt, int Smax, bf16_t* v_rows,
+                                                  const int32_t* skip) {
+    if (skip && *skip) return;
+    const int row = blockIdx.x;   // r*S + t
+    const int r = row / S, t = row % S;
+    const int pos = pos0 + t + (pos_dev ? *pos_dev : 0);
+    const int N = (H + 2 * Hkv) * hd;
+    const size_t slab = (size_t)R * S * N;
+    const float* p = part + (size_t)row * N;
+    const float* fc = freqs + (size_t)pos * hd;     // [hd/2][2]
+    for (int pi = threadIdx.x; pi < N / 2; pi += blockDim.x) {
+        const int col = 2 * pi;
+        float a = p[col], bb = p[col + 1];
+        for (int s = 1; s < nsplit; ++s) { a += p[s * slab + col]; bb += p[s * slab + col + 1]; }
+        a = round_bf(a); bb = round_bf(bb);
+        const int d = col % hd;
+        if (col < (H + Hkv) * hd) {
+            const float c = fc[d], sn = fc[d + 1];   // pair index d/2 -> (cos, sin) at [d/2][0..1]
+            const float o0 = __fsub_rn(__fmul_rn(a, c), __fmul_rn(bb, sn));
+            const float o1 = __fadd_rn(__fmul_rn(bb, c), __fmul_rn(a, sn));
+            const uint32_t pk = pack2(o0, o1);
+            if (col < H * hd) {
+                *reinterpret_cast<uint32_t*>(q_out + (size_t)row * H * hd + col) = pk;
+            } else {
+                const int g = (col - H * hd) / hd;
+                *reinterpret_cast<uint32_t*>(kc + (((size_t)r * Hkv + g) * Smax + pos) * hd + d) = pk;
+            }
+        } else {
+            const int g = (col - (H + Hkv) * hd) / hd;
+            bf16_t* base = vt + (((size_t)r * Hkv + g) * hd + d) * Smax + pos;
+            const bf16_t va = f2bf(a), vb = f2bf(bb);
+            base[0] = va;
+            base[Smax] = vb;
+            if (v_rows) {
+                *reinterpret_cast<uint32_t*>(v_rows + (((size_t)r * Hkv + g) * S + t) * hd + d) =
+                    (uint32_t)va | ((uint32_t)vb << 16);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ decode attention
+constexpr int AT_CH = 256;      // keys per workgroup (4 waves x 64)
+constexpr int AT_G = 4;         // query heads per KV head handled by the B operand (<= 16)
+
+// work layout per (r, g, split): [G] max, [G] sum, [G][hd] unnormalised output
+__global__ __launch_bounds__(256) void k_attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vt, int R,
+                                                     int H, int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
+                                                     float* work, int max_splits, float scale,
+                                                     const int32_t* skip) {
+    constexpr int HD = 128;
+    __shared__ float s_m[4][16];
+    __shared__ float s_l[4][16];
+    __shared__ float s_o[4][AT_G][HD];
+    if (skip && *skip) return;
+    const int split = blockIdx.x, g = blockIdx.y, r = blockIdx.z;
+    const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
+    const int nsplit = (ctx + AT_CH - 1) / AT_CH;
+    if (split >= nsplit) return;
+    const int G = H / Hkv;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n = lane & 15, grp = lane >> 4;
+    const int key0 = split * AT_CH + w * 64;
+
+    // Q^T fragments (B operand): B[k = d][n = head]
+    bf16x8 qf[4];
+    {
+        const bf16_t* qr = q + (size_t)r * H * HD + (size_t)(g * G + n) * HD;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (n < G) v = *reinterpret_cast<const uint4*>(qr + ks * 32 + grp * 8);
+            qf[ks] = as_frag(v);
+        }
+    }
+    const bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
+    const bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
+
+    // ---- S^T = K . Q^T for 64 keys (4 tiles of 16)
+    uint4 kf[4][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            kf[kt][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)(key0 + kt * 16 + n) * HD + ks * 32 + grp * 8);
+    // V^T fragments for the two 32-key steps: keys 32u + 4grp + {0..3} and 32u + 16 + 4grp + {0..3}
+    uint2 vf[2][8][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            const bf16_t* vrow = vb + (size_t)(dt * 16 + n) * Smax + key0 + 32 * u + 4 * grp;
+            vf[u][dt][0] = *reinterpret_cast<const uint2*>(vrow);
+            vf[u][dt][1] = *reinterpret_cast<const uint2*>(vrow + 16);
+        }
+    f32x4 sacc[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+        sacc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            sacc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(kf[kt][ks]), qf[ks], sacc[kt], 0, 0, 0);
+    }
+    // scores: key = key0 + 16kt + 4grp + i, head = n
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int key = key0 + kt * 16 + grp * 4 + i;
+            float sv = sacc[kt][i] * scale;
+            if (key >= ctx) sv = -INFINITY;
+            sacc[kt][i] = sv;
+            m = fmaxf(m, sv);
+        }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    if (grp == 0) s_m[w][n] = m;
+    __syncthreads();
+    const float M = fmaxf(fmaxf(s_m[0][n], s_m[1][n]), fmaxf(s_m[2][n], s_m[3][n]));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float pv = (M == -INFINITY) ? 0.f : __expf(sacc[kt][i] - M);
+            sacc[kt][i] = pv;
+            l += pv;
+        }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (grp == 0) s_l[w][n] = l;
+
+    // ---- O = P . V : A = P[head][key], k-index kk=8grp+j <-> local key 32u + (j<4 ? 4grp+j : 16+4grp+j-4)
+    f32x4 oacc[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const f32x4 p0 = sacc[2 * u], p1 = sacc[2 * u + 1];
+        const uint4 pa = make_uint4(pack2(p0[0], p0[1]), pack2(p0[2], p0[3]), pack2(p1[0], p1[1]),
+                                    pack2(p1[2], p1[3]));
+        // A operand needs row = head (= n), but the scores sit at column n: transpose via the
+        // MFMA: use P^T as the B operand instead and V^T as the A operand -> O^T[d][head].
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            const uint4 va = make_uint4(vf[u][dt][0].x, vf[u][dt][0].y, vf[u][dt][1].x, vf[u][dt][1].y);
+            oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(va), as_frag(pa), oacc[dt], 0, 0, 0);
+        }
+    }
+    // oacc[dt][i] = O^T[d = dt*16 + 4grp + i][head = n]
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (n < AT_G) s_o[w][n][dt * 16 + grp * 4 + i] = oacc[dt][i];
+    __syncthreads();
+    // reduce the 4 waves and write the split's partial result
+    float* wp = work + (((size_t)r * Hkv + g) * max_splits + split) * (2 * AT_G + AT_G * HD);
+    for (int i = threadIdx.x; i < AT_G * HD; i += 256) {
+        const int h = i / HD, d = i % HD;
+        wp[2 * AT_G + i] = s_o[0][h][d] + s_o[1][h][d] + s_o[2][h][d] + s_o[3][h][d];
+    }
+    if (threadIdx.x < AT_G) {
+        const int h = threadIdx.x;
+        wp[h] = fmaxf(fmaxf(s_m[0][h], s_m[1][h]), fmaxf(s_m[2][h], s_m[3][h]));
+        wp[AT_G + h] = s_l[0][h] + s_l[1][h] + s_l[2][h] + s_l[3][h];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_attn_combine(const float* work, int H, int Hkv, int max_splits, int ctx0,
+                                                     const int32_t* ctx_dev, bf16_t* out, const int32_t* skip) {
+    constexpr int HD = 128;
+    if (skip && *skip) return;
+    const int h = blockIdx.x, r = blockIdx.y;
+    const int G = H / Hkv, g = h / G, j = h % G;
+    const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
+    const int nsplit = (ctx + AT_CH - 1) / AT_CH;
+    const float* base = work + ((size_t)r * Hkv + g) * max_splits * (2 * AT_G + AT_G * HD);
+    constexpr int STR = 2 * AT_G + AT_G * HD;
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, base[s * STR + j]);
+    float L = 0.f, o0 = 0.f, o1 = 0.f;
+    const int d = threadIdx.x * 2;
+    for (int s = 0; s < nsplit; ++s) {
+        const float* p = base + s * STR;
+        const float c = (p[j] == -INFINITY) ? 0.f : __expf(p[j] - M);
+        L += p[AT_G + j] * c;
+        o0 += p[2 * AT_G + j * HD + d] * c;
+        o1 += p[2 * AT_G + j * HD + d + 1] * c;
+    }
+    const float inv = 1.0f / L;
+    *reinterpret_cast<uint32_t*>(out + (size_t)r * H * HD + (size_t)h * HD + d) = pack2(o0 * inv, o1 * inv);
+}
+
+// ------------------------------------------------------------------ prefill attention (causal)
+// One wave per query (r, h, t); 64-key chunks: lane = key for the scores, lane = 2 channels
+// for the output. K rows and V rows ([R][Hkv][S][hd] scratch written by k_qkv_rope) stream
+// coalesced.
+__global__ __launch_bounds__(256) void k_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vrows, int R,
+                                                      int S, int H, int Hkv, int Smax, float scale, bf16_t* out) {
+    constexpr int HD = 128;
+    __shared__ uint4 sq[4][HD / 8];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int qi = blockIdx.x * 4 + w;          // query index within (r, h)
+    const int h = blockIdx.y, r = blockIdx.z;
+    const bool active = qi < S;
+    const int t = active ? qi : S - 1;
+    const int G = H / Hkv, g = h / G;
+    const bf16_t* qr = q + ((size_t)(r * S + t) * H + h) * HD;
+    if (lane < HD / 8) sq[w][lane] = reinterpret_cast<const uint4*>(qr)[lane];
+    __syncthreads();
+    const bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
+    const bf16_t* vb = vrows + ((size_t)r * Hkv + g) * S * HD;
+    float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+    for (int c0 = 0; c0 <= t; c0 += 64) {
+        const int key = c0 + lane;
+        float sv = -INFINITY;
+        if (key <= t) {
+            float acc = 0.f;
+            const uint4* kr = reinterpret_cast<const uint4*>(kb + (size_t)key * HD);
+#pragma unroll
+            for (int i = 0; i < HD / 8; ++i) {
+                float a[8], bq[8];
+                unpack8(kr[i], a);
+                unpack8(sq[w][i], bq);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc += a[e] * bq[e];
+            }
+            sv = acc * scale;
+        }
+        const float cm = wave_max(sv);
+        const float mn = fmaxf(m, cm);
+        const float corr = (m == -INFINITY) ? 0.f : __expf(m - mn);
+        const float p = (sv == -INFINITY) ? 0.f : __expf(sv - mn);
+        l = l * corr + wave_sum(p);
+        o0 *= corr;
+        o1 *= corr;
+        const int nk = min(64, t + 1 - c0);
+        for (int j = 0; j < nk; ++j) {
+            const float pj = __shfl(p, j, 64);
+            const uint32_t vv = *reinterpret_cast<const uint32_t*>(vb + (size_t)(c0 + j) * HD + 2 * lane);
+            o0 += pj * __uint_as_float(vv << 16);
+            o1 += pj * __uint_as_float(vv & 0xffff0000u);
+        }
+        m = mn;
+    }
+    if (active) {
+        const float inv = 1.0f / l;
+        *reinterpret_cast<uint32_t*>(out + ((size_t)(r * S + t) * H + h) * HD + 2 * lane) = pack2(o0 * inv, o1 * inv);
+    }
+}
+
+}  // namespace
+
+#define ZK_LN_DISPATCH(D, kern, ...)                                              \
+    do {                                                                           \
+        const int _n8 = ((D) / 8 + LN_NT - 1) / LN_NT;                             \
+        if (_n8 == 1) hipLaunchKernelGGL(kern<1>, __VA_ARGS__);                    \
+        else if (_n8 == 2) hipLaunchKernelGGL(kern<2>, __VA_ARGS__);               \
+        else if (_n8 == 3) hipLaunchKernelGGL(kern<3>, __VA_ARGS__);               \
+        else hipLaunchKernelGGL(kern<4>, __VA_ARGS__);                             \
+    } while (0)
+
+extern "C" int zk_embed_codes(const int64_t* ids, int B, int S, int K, long ids_bstride, long ids_kstride,
+                              const int32_t* col_dev, int col_add, const void* emb, int V, int D, int rows_dup,
+                              void* x_out, int out_S, int out_t0, const void* ln_w, const void* ln_b, float eps,
+                              void* xn_out, const int32_t* skip, void* stream) {
+    ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_embed_codes: D=%d must be a multiple of 8 (<= %d)", D,
+               8 * LN_NT * MAX_N8);
+    ZK_REQUIRE(B > 0 && S > 0 && K > 0 && rows_dup > 0, "zk_embed_codes: empty shape");
+    const int rows = rows_dup * B * S;
+    ZK_REQUIRE(out_S >= out_t0 + S, "zk_embed_codes: out_S=%d < out_t0+S", out_S);
+    ZK_LN_DISPATCH(D, k_embed_ln, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, ids, B, S, K, ids_bstride,
+                   ids_kstride, col_dev, col_add, (const bf16_t*)emb, V, D, (bf16_t*)x_out, out_S, out_t0,
+                   (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, (bf16_t*)xn_out, skip);
+    ZK_CHECK_LAUNCH("zk_embed_codes");
+    return 0;
+}
+
+extern "C" int zk_layernorm(const void* x, const void* w, const void* b, float eps, int rows, int D, void* y,
+                            void* stream) {
+    ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_layernorm: unsupported D=%d", D);
+    if (rows == 0) return 0;
+    ZK_LN_DISPATCH(D, k_layernorm, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       (const bf16_t*)w, (const bf16_t*)b, eps, D, (bf16_t*)y);
+    ZK_CHECK_LAUNCH("zk_layernorm");
+    return 0;
+}
+
+extern "C" int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, const void* b, float eps,
+                           int rows, int D, void* x_out, void* xn_out, const int32_t* skip, void* stream) {
+    ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_resid_ln: unsupported D=%d", D);
+    ZK_REQUIRE(nsplit >= 1, "zk_resid_ln: nsplit must be >= 1");
+    if (rows == 0) return 0;
+    ZK_LN_DISPATCH(D, k_resid_ln, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, part, nsplit,
+                       (const bf16_t*)x_in, (const bf16_t*)w, (const bf16_t*)b, eps, rows, D, (bf16_t*)x_out,
+                       (bf16_t*)xn_out, skip);
+    ZK_CHECK_LAUNCH("zk_resid_ln");
+    return 0;
+}
+
+extern "C" int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv, int hd, const float* freqs,
+                           int pos0, const int32_t* pos_dev, void* q_out, void* k_cache, void* vt_cache, int Smax,
+                           void* v_rows, const int32_t* skip, void* stream) {
+    ZK_REQUIRE(hd % 2 == 0 && nsplit >= 1, "zk_qkv_rope: bad args");
+    if (R * S == 0) return 0;
+    hipLaunchKernelGGL(k_qkv_rope, dim3(R * S), dim3(256), 0, (hipStream_t)stream, part, nsplit, R, S, H, Hkv, hd,
+                       freqs, pos0, pos_dev, (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)vt_cache, Smax,
+                       (bf16_t*)v_rows, skip);
+    ZK_CHECK_LAUNCH("zk_qkv_rope");
+    return 0;
+}
+
+extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt_cache, int R, int H, int Hkv,
+                              int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int max_splits,
+                              void* out, const int32_t* skip, void* stream) {
+    ZK_REQUIRE(hd == 128, "zk_attn_decode: head_dim %d unsupported (128 only)", hd);
+    ZK_REQUIRE(H % Hkv == 0 && H / Hkv <= AT_G, "zk_attn_decode: GQA group %d > %d", H / Hkv, AT_G);
+    ZK_REQUIRE(Smax % AT_CH == 0 && max_splits * AT_CH >= Smax,
+               "zk_attn_decode: Smax=%d must be a multiple of %d covered by max_splits=%d", Smax, AT_CH, max_splits);
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipLaunchKernelGGL(k_attn_decode, dim3(max_splits, Hkv, R), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0,
+                       ctx_dev, work, max_splits, scale, skip);
+    ZK_CHECK_LAUNCH("zk_attn_decode");
+    hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, max_splits, ctx0,
+                       ctx_dev, (bf16_t*)out, skip);
+    ZK_CHECK_LAUNCH("zk_attn_combine");
+    return 0;
+}
+
+extern "C" int zk_attn_prefill(const void* q, const void* k_cache, const void* v_rows, int R, int S, int H, int Hkv,
+                               int hd, int Smax, void* out, void* stream) {
+    ZK_REQUIRE(hd == 128, "zk_attn_prefill: head_dim %d unsupported (128 only)", hd);
+    ZK_REQUIRE(H % Hkv == 0, "zk_attn_prefill: H %% Hkv != 0");
+    if (R * S == 0) return 0;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipLaunchKernelGGL(k_attn_prefill, dim3((S + 3) / 4, H, R), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_rows, R, S, H, Hkv, Smax, scale,
+                       (bf16_t*)out);
+    ZK_CHECK_LAUNCH("zk_attn_prefill");
+    return 0;
+}

@@ -1,0 +1,98 @@
+// Shared device helpers for the Zonos MI355X (gfx950) kernels.
+// Wave = 64 lanes everywhere; all reductions are written for wave64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ZK_DEV __device__ __forceinline__
+
+typedef uint16_t bf16_t;   // raw bf16 bits (torch.bfloat16 storage)
+typedef uint16_t f16_t;
+
+// ---------------------------------------------------------------- bf16 <-> f32
+// Round-to-nearest-even exactly like torch's float->bfloat16 conversion (c10/util/BFloat16.h),
+// NaN kept as a quiet NaN.
+ZK_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+ZK_DEV bf16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)0x7fc0;
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+ZK_DEV float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// Unpack 8 bf16 held in a uint4 (16 B) to floats.
+ZK_DEV void unpack8(const uint4 v, float* f) {
+    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+    f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+    f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+ZK_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+ZK_DEV uint4 pack8(const float* f) {
+    return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+// ---------------------------------------------------------------- wave64 reductions
+ZK_DEV float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+ZK_DEV double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+ZK_DEV float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Block-wide reductions for blocks of NT threads (NT multiple of 64, <= 1024).
+// `red` is NT/64 floats of LDS scratch. All threads receive the result.
+template <int NT>
+ZK_DEV float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    return t;
+}
+template <int NT>
+ZK_DEV float block_max(float v, float* red) {
+    v = wave_max(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float t = red[0];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) t = fmaxf(t, red[i]);
+    return t;
+}
+
+// ---------------------------------------------------------------- host-side error plumbing
+#ifdef __cplusplus
+extern "C" void zk_set_error(const char* fmt, ...);
+#endif
+#define ZK_CHECK_LAUNCH(name)                                                  \
+    do {                                                                       \
+        hipError_t _e = hipGetLastError();                                     \
+        if (_e != hipSuccess) {                                                \
+            zk_set_error("%s: launch failed: %s", name, hipGetErrorString(_e)); \
+            return -1;                                                         \
+        }                                                                      \
+    } while (0)
+#define ZK_REQUIRE(cond, ...)           \
+    do {                                \
+        if (!(cond)) {                  \
+            zk_set_error(__VA_ARGS__);  \
+            return -2;                  \
+        }                               \
+    } while (0)

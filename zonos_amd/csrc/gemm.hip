@@ -1,0 +1,176 @@
+// bf16 "nn.Linear" GEMM for gfx950: C[M][N] = A[M][K] . W[N][K]^T, fp32 accumulation on
+// MFMA 16x16x32 bf16.
+//
+// Shape of the work: the decode step multiplies 2B = 128 activation rows by weight
+// matrices streamed once from HBM (3.2 GB of weights per step), so the
+// tile is 128 rows x 64 columns: every row of the batch lives in one workgroup and each
+// weight element is read exactly once per step. 4 waves; wave w owns 16 weight rows
+// (output columns) and all 128 activation rows, so its B fragments come straight from
+// HBM into registers (no LDS round trip for the once-read stream) while the activation
+// tile -- re-read by every column tile, L2-resident -- is staged in LDS (XOR-swizzled,
+// double-buffered, 64-deep K chunks). Split-K over gridDim.z fills the 256 CUs when N is
+// small; the partial slabs are reduced by the consumer kernel (k_resid_ln / k_qkv_rope /
+// the sampler), in a fixed order, so results do not depend on M (batch-invariant).
+//
+// mode 0: fp32 partial slabs; mode 1: fused SwiGLU for FeedForward.fc1 (_torch.py:150-152).
+#include "common.h"
+#include "../../include/zonos_hip.h"
+#include <algorithm>
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int BM = 128, BN = 64, BK = 64, NT = 256;
+
+ZK_DEV bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// LDS byte offset of 16-byte chunk c (0..7) of tile row `row` (128-byte rows, XOR swizzle)
+ZK_DEV int lds_off(int row, int c) { return row * 128 + ((c ^ (row & 7)) << 4); }
+
+template <int MODE>
+__global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ W,
+                                             int M, int N, int K, int kslice, float* __restrict__ Cpart,
+                                             bf16_t* __restrict__ Cout, const int32_t* skip) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * BM * BK * 2];
+    if (skip && *skip) return;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, split = blockIdx.z;
+    const int kbeg = split * kslice;
+    const int nchunks = kslice / BK;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ln = lane & 15, lg = lane >> 4;
+
+    // this lane's weight row
+    const int wn = n0 + w * 16 + ln;
+    const bool wvalid = wn < N;
+    const bf16_t* wrow = W + (size_t)(wvalid ? wn : 0) * K + kbeg + lg * 8;
+
+    // activation staging: 4 chunks of 16 B per thread per K chunk
+    uint4 areg[4];
+    auto load_a = [&](int ch) {
+        const int k0 = kbeg + ch * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = tid + NT * i;
+            const int row = q >> 3, c = q & 7;
+            const int m = m0 + row;
+            areg[i] = (m < M) ? *reinterpret_cast<const uint4*>(A + (size_t)m * lda + k0 + c * 8)
+                              : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_a = [&](int buf) {
+        char* base = smem + buf * (BM * BK * 2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = tid + NT * i;
+            *reinterpret_cast<uint4*>(base + lds_off(q >> 3, q & 7)) = areg[i];
+        }
+    };
+    auto load_w = [&](int ch, uint4* wf) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+            wf[ks] = wvalid ? *reinterpret_cast<const uint4*>(wrow + ch * BK + ks * 32) : make_uint4(0, 0, 0, 0);
+    };
+
+    f32x4 acc[8];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    uint4 wc[2], wn_[2];
+    load_a(0);
+    load_w(0, wc);
+    store_a(0);
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int cur = ch & 1;
+        const bool more = ch + 1 < nchunks;
+        if (more) {
+            load_a(ch + 1);
+            load_w(ch + 1, wn_);
+        }
+        const char* base = smem + cur * (BM * BK * 2);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const bf16x8 b = as_frag(wc[ks]);
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
+            }
+        }
+        if (more) {
+            store_a(cur ^ 1);
+            wc[0] = wn_[0];
+            wc[1] = wn_[1];
+        }
+        __syncthreads();
+    }
+
+    // epilogue: acc[mt][i] = C[m0 + 16mt + 4lg + i][wn]
+    if (MODE == 0) {
+        float* C = Cpart + (size_t)split * M * N;
+        if (wvalid) {
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = m0 + mt * 16 + lg * 4 + i;
+                    if (m < M) C[(size_t)m * N + wn] = acc[mt][i];
+                }
+        }
+    } else {
+        // interleaved fc1 rows: within each group of 16 columns, 0..7 = y[f0..f0+7], 8..15 = gate[f0..]
+        const int F = N / 2;
+        const int f = (n0 + w * 16) / 2 + (ln & 7);
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float mine = round_bf(acc[mt][i]);
+                const float other = __shfl_xor(mine, 8, 64);
+                const int m = m0 + mt * 16 + lg * 4 + i;
+                if (ln < 8 && m < M && f < F) {
+                    const float y = mine, g = other;
+                    const float sl = round_bf(g / (1.0f + expf(-g)));     // F.silu in bf16
+                    Cout[(size_t)m * F + f] = f2bf(y * sl);
+                }
+            }
+    }
+}
+
+__global__ void k_permute_fc1(const bf16_t* w, int F, int D, bf16_t* out) {
+    const int nr = blockIdx.x;         // new row
+    const int q = nr / 16, j = nr % 16;
+    const int src = (j < 8) ? (q * 8 + j) : (F + q * 8 + (j - 8));
+    const uint4* s = reinterpret_cast<const uint4*>(w + (size_t)src * D);
+    uint4* d = reinterpret_cast<uint4*>(out + (size_t)nr * D);
+    for (int i = threadIdx.x; i < D / 8; i += blockDim.x) d[i] = s[i];
+}
+
+}  // namespace
+
+extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
+                            float* Cpart, void* Cout, const int32_t* skip_flag, void* stream) {
+    ZK_REQUIRE(M > 0 && N > 0 && K > 0, "zk_gemm_bf16: empty shape M=%d N=%d K=%d", M, N, K);
+    ZK_REQUIRE(nsplit >= 1 && K % (nsplit * BK) == 0, "zk_gemm_bf16: K=%d must be a multiple of nsplit*%d", K, BK);
+    ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemm_bf16: lda=%ld", lda);
+    ZK_REQUIRE(mode == 0 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_bf16: bad mode/nsplit");
+    dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nsplit);
+    if (mode == 0)
+        hipLaunchKernelGGL(k_gemm<0>, grid, dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)A, lda,
+                           (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout, skip_flag);
+    else
+        hipLaunchKernelGGL(k_gemm<1>, grid, dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)A, lda,
+                           (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout, skip_flag);
+    ZK_CHECK_LAUNCH("zk_gemm_bf16");
+    return 0;
+}
+
+extern "C" int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream) {
+    ZK_REQUIRE(F % 8 == 0 && D % 8 == 0, "zk_permute_fc1: F=%d D=%d", F, D);
+    hipLaunchKernelGGL(k_permute_fc1, dim3(2 * F), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)w_fc1, F, D,
+                       (bf16_t*)w_out);
+    ZK_CHECK_LAUNCH("zk_permute_fc1");
+    return 0;
+}

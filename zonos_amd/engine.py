@@ -1,0 +1,377 @@
+"""The MI355X decode engine: Zonos.generate()'s hot loop on hand-written HIP kernels.
+
+Restates zonos/model.py:224-457 (generate) with the transformer backbone of
+zonos/backbone/_torch.py, the heads/CFG of model.py:100-116, the sampler of
+zonos/sampling.py and the delay pattern of zonos/codebook_pattern.py.
+
+Design (MI355X-first):
+  * All per-step state (offset, position, EOS protocol, repetition penalty, delayed
+    codes) lives on the device; one decode step = a fixed launch sequence with no host
+    synchronisation, captured once into a hipGraph and replayed in chunks of
+    `poll_every` steps. The host polls a `done` word between chunks; steps after
+    completion are no-ops (every kernel checks the word).
+  * Weights are bf16 in HBM in the engine's layouts: 9 embedding tables stacked
+    [9][1026][D], the 9 heads stacked [9*1026][D], fc1 rows interleaved for the fused
+    SwiGLU epilogue. The KV cache is [R][Hkv][Smax][hd] (K) + [R][Hkv][hd][Smax] (V^T).
+  * torch is plumbing only: it allocates device memory and provides the stream.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import GenState, SamplingParams, call, ptr
+
+EOS, MASK, UNKNOWN = 1024, 1025, -1
+N_CB = 9
+VOCAB = 1026
+ATTN_CHUNK = 256
+
+
+@dataclass
+class EngineConfig:
+    d_model: int
+    n_layer: int
+    n_heads: int
+    n_kv: int
+    d_ff: int
+    eps: float = 1e-5
+
+    @property
+    def head_dim(self):
+        return self.d_model // self.n_heads
+
+    @classmethod
+    def from_backbone_config(cls, bc) -> "EngineConfig":
+        return cls(d_model=bc.d_model, n_layer=bc.n_layer, n_heads=bc.attn_cfg["num_heads"],
+                   n_kv=bc.attn_cfg["num_heads_kv"], d_ff=bc.attn_mlp_d_intermediate, eps=bc.norm_epsilon)
+
+
+def rope_table(seq_len: int, head_dim: int, base: float = 10000.0) -> torch.Tensor:
+    """precompute_freqs_cis (_torch.py:9-15), computed on the host CPU exactly as the
+    reference does, then uploaded: [seq_len][hd/2][2] fp32 (cos, sin)."""
+    inv = 1.0 / (base ** (torch.arange(0, head_dim, 2)[: head_dim // 2].float() / head_dim))
+    ang = torch.outer(torch.arange(seq_len, device=inv.device), inv)
+    z = torch.polar(torch.ones_like(ang), ang)
+    return torch.stack([z.real, z.imag], dim=-1).contiguous()
+
+
+def _split_for(N: int, K: int, M: int, target_blocks: int = 256) -> int:
+    """Split-K count for the 128x64-tile GEMM: enough workgroups to cover the CUs.
+    Depends on (N, K) only for M <= 128 so the reduction order is batch-invariant."""
+    if M > 128:
+        return 1
+    tiles = (N + 63) // 64
+    want = max(1, math.ceil(target_blocks / tiles))
+    s = 1
+    for cand in range(1, want + 1):
+        if K % (cand * 64) == 0:
+            s = cand
+    return s
+
+
+class HipDecoder:
+    """Owns device weights in engine layout and runs generate() on the GPU."""
+
+    def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
+        _lib.load()
+        self.cfg = cfg
+        self.device = torch.device(device)
+        c = cfg
+        bf = torch.bfloat16
+        dev = self.device
+
+        def w(name):
+            t = weights[name]
+            return t.to(device=dev, dtype=bf).contiguous()
+
+        self.emb = torch.stack([w(f"embeddings.{k}.weight") for k in range(N_CB)]).contiguous()
+        assert self.emb.shape == (N_CB, VOCAB, c.d_model), self.emb.shape
+        heads = []
+        for k in range(N_CB):
+            h = w(f"heads.{k}.weight")
+            if h.shape[0] < VOCAB:      # pad_weight_ (utils.py:22-37): 1025 -> 1026 rows
+                h = torch.cat([h, h.new_zeros(VOCAB - h.shape[0], h.shape[1])])
+            heads.append(h)
+        self.heads = torch.cat(heads).contiguous()          # [9*1026][D]
+        self.layers = []
+        stream = _lib.stream_ptr(dev)
+        for i in range(c.n_layer):
+            p = f"backbone.layers.{i}."
+            fc1 = w(p + "mlp.fc1.weight")
+            fc1p = torch.empty_like(fc1)
+            call("zk_permute_fc1", ptr(fc1), c.d_ff, c.d_model, ptr(fc1p), stream)
+            self.layers.append(dict(
+                ln1_w=w(p + "norm.weight"), ln1_b=w(p + "norm.bias"),
+                wqkv=w(p + "mixer.in_proj.weight"), wo=w(p + "mixer.out_proj.weight"),
+                ln2_w=w(p + "norm2.weight"), ln2_b=w(p + "norm2.bias"),
+                fc1=fc1p, fc2=w(p + "mlp.fc2.weight")))
+        self.lnf_w = w("backbone.norm_f.weight")
+        self.lnf_b = w("backbone.norm_f.bias")
+        self.freqs = rope_table(16384, c.head_dim).to(dev)
+        self._ws = None
+        torch.cuda.synchronize(dev)
+
+    # ------------------------------------------------------------------ workspace
+    def _alloc(self, B: int, Lc: int, P: int, max_new: int):
+        c = self.cfg
+        dev = self.device
+        R = 2 * B
+        T = P + max_new
+        Ld = T + N_CB
+        seq_len = Lc + T + N_CB
+        smax = -(-seq_len // ATTN_CHUNK) * ATTN_CHUNK
+        S_pre = Lc + P + 1
+        key = (B, Lc, P, max_new)
+        if self._ws is not None and self._ws["key"] == key:
+            ws = self._ws
+            ws["kv"].zero_()
+            return ws
+        self.release()
+        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+        Nqkv = (H + 2 * Hk) * hd
+        Nh = N_CB * VOCAB
+        Mp = R * S_pre
+        f32, bf, i32 = torch.float32, torch.bfloat16, torch.int32
+        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R), fc2=_split_for(D, Fd, R),
+                      heads=_split_for(Nh, D, R))
+        part_n = max(Mp * Nqkv, Mp * D, splits["qkv"] * R * Nqkv, splits["o"] * R * D, splits["fc2"] * R * D,
+                     splits["heads"] * R * Nh)
+        max_splits = smax // ATTN_CHUNK
+        ws = dict(
+            key=key, R=R, T=T, Ld=Ld, smax=smax, S_pre=S_pre, splits=splits, max_splits=max_splits,
+            kv=torch.zeros(c.n_layer, 2, R * Hk * smax * hd, dtype=bf, device=dev),
+            x=torch.empty(Mp, D, dtype=bf, device=dev), xn=torch.empty(Mp, D, dtype=bf, device=dev),
+            q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
+            h=torch.empty(Mp, Fd, dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
+            vrows=torch.empty(R * Hk * S_pre * hd, dtype=bf, device=dev),
+            attn_work=torch.empty(R * Hk * max_splits * (8 + 4 * hd), dtype=f32, device=dev),
+            scal=torch.zeros(16, dtype=i32, device=dev),
+            eos_mode=torch.zeros(B, dtype=i32, device=dev), steps_after=torch.zeros(B, dtype=i32, device=dev),
+            remaining=torch.zeros(B, dtype=i32, device=dev), stopping=torch.zeros(B, dtype=i32, device=dev),
+            act=torch.zeros(B, dtype=i32, device=dev), rp=torch.ones(B, dtype=f32, device=dev),
+            tok0=torch.zeros(B * N_CB, dtype=i32, device=dev), tok1=torch.zeros(B * N_CB, dtype=i32, device=dev),
+            delayed=torch.empty(B, N_CB, Ld, dtype=torch.int64, device=dev),
+            dbg=torch.empty(B, N_CB, VOCAB, dtype=f32, device=dev),
+            graph=None,
+        )
+        self._ws = ws
+        return ws
+
+    def release(self):
+        if self._ws is not None and self._ws.get("graph"):
+            call("zk_graph_destroy", self._ws["graph"])
+        self._ws = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+    def _kv(self, ws, layer):
+        return ws["kv"][layer, 0], ws["kv"][layer, 1]
+
+    # ------------------------------------------------------------------ transformer passes
+    def _layers(self, ws, M: int, R: int, S: int, prefill: bool, stream, skip):
+        """Run the 26 blocks on xn/x (rows = R*S). Leaves norm_f(x) in ws['xn']."""
+        c = self.cfg
+        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+        Nqkv = (H + 2 * Hk) * hd
+        sp = ws["splits"] if not prefill else dict(qkv=1, o=1, fc2=1)
+        x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
+        scal = ws["scal"]
+        pos_dev = None if prefill else ptr(scal[1:2])
+        for i, L in enumerate(self.layers):
+            kc, vt = self._kv(ws, i)
+            call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
+            call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q), ptr(kc),
+                 ptr(vt), ws["smax"], ptr(ws["vrows"]) if prefill else None, skip, stream)
+            if prefill:
+                call("zk_attn_prefill", ptr(q), ptr(kc), ptr(ws["vrows"]), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
+            else:
+                call("zk_attn_decode", ptr(q), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1, ptr(scal[1:2]),
+                     ptr(ws["attn_work"]), ws["max_splits"], ptr(y), skip, stream)
+            call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip, stream)
+            call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D, ptr(x),
+                 ptr(xn), skip, stream)
+            call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fd, D, 1, 1, None, ptr(h), skip, stream)
+            call("zk_gemm_bf16", ptr(h), Fd, ptr(L["fc2"]), M, D, Fd, sp["fc2"], 0, ptr(part), None, skip, stream)
+            if i + 1 < len(self.layers):
+                nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
+            else:
+                nw, nb = self.lnf_w, self.lnf_b
+            call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), skip,
+                 stream)
+
+    def _heads(self, ws, R: int, S: int, stream, skip):
+        """Heads GEMM on the last position of every row -> split-K slabs in ws['part']."""
+        D = self.cfg.d_model
+        last = ws["xn"][S - 1:]           # rows r*S + S-1 via lda = S*D
+        call("zk_gemm_bf16", ptr(last), S * D, ptr(self.heads), R, N_CB * VOCAB, D, ws["splits"]["heads"], 0,
+             ptr(ws["part"]), None, skip, stream)
+
+    def _gen_state(self, ws, B, seed, row_base) -> GenState:
+        return GenState(ptr(ws["scal"]), ptr(ws["eos_mode"]), ptr(ws["steps_after"]), ptr(ws["remaining"]),
+                        ptr(ws["stopping"]), ptr(ws["act"]), ptr(ws["rp"]), ptr(ws["tok0"]), ptr(ws["tok1"]),
+                        ptr(ws["delayed"]), B, N_CB, ws["Ld"], VOCAB, seed & 0xFFFFFFFFFFFFFFFF, row_base)
+
+    def _decode_step(self, ws, B, st, sp, stream):
+        c = self.cfg
+        R = 2 * B
+        scal = ws["scal"]
+        skip = ptr(scal[3:4])
+        L0 = self.layers[0]
+        call("zk_embed_codes", ptr(ws["delayed"]), B, 1, N_CB, ws["Ld"] * N_CB, ws["Ld"], ptr(scal[0:1]), -1,
+             ptr(self.emb), VOCAB, c.d_model, 2, ptr(ws["x"]), 1, 0, ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps,
+             ptr(ws["xn"]), skip, stream)
+        self._layers(ws, R, R, 1, False, stream, skip)
+        self._heads(ws, R, 1, stream, skip)
+        nsp = ws["splits"]["heads"]
+        call("zk_sample_heads", ptr(ws["part"]), nsp, C_ref(st), C_ref(sp), 0, 0, ptr(ws["dbg"]), stream)
+        call("zk_sample_heads", ptr(ws["part"]), nsp, C_ref(st), C_ref(sp), 0, 1, None, stream)
+        call("zk_eos_step", C_ref(st), 0, 0, stream)
+
+    # ------------------------------------------------------------------ generate
+    @torch.inference_mode()
+    def generate(self, prefix_conditioning: torch.Tensor, audio_prefix_codes=None, max_new_tokens: int = 86 * 30,
+                 cfg_scale: float = 2.0, batch_size: int = 1, sampling_params: dict | None = None,
+                 seed: int = 0, row_base: int = 0, force_full_length: bool = False, callback=None,
+                 progress=None, poll_every: int = 16, trace: dict | None = None, use_graph: bool = True):
+        """Zonos.generate (model.py:224-457). Returns the list of int64 [9, T_i] code tensors.
+
+        ``trace`` (optional dict) receives per-step fp32 CFG logits (before bias) and the
+        sampled frames -- test instrumentation, forces one step per poll and no graph."""
+        assert cfg_scale != 1, "TODO: add support for cfg_scale=1"                     # model.py:247
+        if batch_size * 2 != prefix_conditioning.shape[0]:                            # model.py:249-250
+            raise ValueError(f"Batch size mismatch: {batch_size} * 2 != {prefix_conditioning.shape[0]}")
+        _lib.require_gpu(prefix_conditioning, "prefix_conditioning")
+        spd = dict(top_p=0, top_k=0, min_p=0, linear=0.55, conf=0.4, quad=0.0, repetition_penalty=3.0,
+                   repetition_penalty_window=2, temperature=1.0)
+        spd.update(sampling_params or {})
+        c = self.cfg
+        B = batch_size
+        R = 2 * B
+        P = 0 if audio_prefix_codes is None else int(audio_prefix_codes.shape[2])
+        Lc = int(prefix_conditioning.shape[1])
+        ws = self._alloc(B, Lc, P, max_new_tokens)
+        stream = _lib.stream_ptr(self.device)
+        T, Ld, S = ws["T"], ws["Ld"], ws["S_pre"]
+        D = c.d_model
+
+        # codes -> delayed codes on device (model.py:288-295)
+        codes = torch.full((B, N_CB, T), UNKNOWN, dtype=torch.int64, device=self.device)
+        if audio_prefix_codes is not None:
+            codes[..., :P] = audio_prefix_codes.to(self.device)
+        call("zk_delay_apply", ptr(codes), B, N_CB, T, MASK, ptr(ws["delayed"]), stream)
+
+        sp = SamplingParams(float(spd["temperature"]), float(spd["top_p"]), float(spd["min_p"]),
+                            float(spd["linear"]), float(spd["conf"]), float(spd["quad"]), int(spd["top_k"]),
+                            int(spd["repetition_penalty_window"]), float(cfg_scale), int(force_full_length))
+        st = self._gen_state(ws, B, seed, row_base)
+        ws["scal"].zero_()
+
+        # ---- prefill (model.py:297-319, _prefill 181-202)
+        x = ws["x"][: R * S].view(R, S, D)
+        x[:, :Lc].copy_(prefix_conditioning.to(torch.bfloat16))
+        call("zk_embed_codes", ptr(ws["delayed"]), B, P + 1, N_CB, Ld * N_CB, Ld, None, 0, ptr(self.emb), VOCAB, D,
+             2, ptr(ws["x"]), S, Lc, None, None, c.eps, None, None, stream)
+        L0 = self.layers[0]
+        call("zk_layernorm", ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, R * S, D, ptr(ws["xn"]), stream)
+        self._layers(ws, R * S, R, S, True, stream, None)
+        self._heads(ws, R, S, stream, None)
+        call("zk_sample_heads", ptr(ws["part"]), ws["splits"]["heads"], C_ref(st), C_ref(sp), 1, 0, ptr(ws["dbg"]),
+             stream)
+        call("zk_eos_step", C_ref(st), 1, P + 1, stream)
+        if trace is not None:
+            trace.setdefault("logits", []).append(ws["dbg"].clone())
+            trace.setdefault("tokens", []).append(ws["tok0"].view(B, N_CB, 1).long().clone())
+
+        # ---- state for the loop (model.py:316-342)
+        max_steps = Ld - (P + 1)
+        ws["scal"].copy_(torch.tensor([P + 2, S, 1, 0, 0, max_steps] + [0] * 10, dtype=torch.int32))
+        ws["eos_mode"].zero_()
+        ws["steps_after"].fill_(6)
+        ws["remaining"].fill_(max_steps)
+        ws["stopping"].zero_()
+        ws["act"].zero_()
+        ws["rp"].fill_(float(spd["repetition_penalty"]))
+
+        # ---- decode loop (model.py:345-432)
+        per_poll = 1 if (callback is not None or trace is not None) else max(1, poll_every)
+        graph = None
+        if use_graph and trace is None:
+            graph = self._capture(ws, B, st, sp, stream)
+        done_steps = 0
+        while True:
+            n = min(per_poll, max_steps - done_steps)
+            if n <= 0:
+                break
+            if graph is not None:
+                call("zk_graph_launch", graph, n, stream)
+            else:
+                for _ in range(n):
+                    self._decode_step(ws, B, st, sp, stream)
+            done_steps += n
+            if trace is not None:
+                trace["logits"].append(ws["dbg"].clone())
+            scal = ws["scal"].cpu()
+            if progress is not None:
+                progress.update(n)
+            if callback is not None:
+                off = int(scal[0]) - 1
+                frame = ws["delayed"][..., off:off + 1]
+                if not callback(frame, done_steps, max_steps):
+                    break
+            if trace is not None:
+                off = int(scal[0]) - 1
+                trace["tokens"].append(ws["delayed"][..., off:off + 1].clone())
+            if int(scal[3]):
+                break
+        offset = int(ws["scal"][0].item()) - 1
+        if trace is not None:
+            trace["delayed"] = ws["delayed"].clone()
+            trace["offset"] = offset
+        return finalize(ws["delayed"], offset, P, stream)
+
+    def _capture(self, ws, B, st, sp, stream):
+        if ws.get("graph"):
+            call("zk_graph_destroy", ws["graph"])
+            ws["graph"] = None
+        # capture on a side stream (torch's default stream cannot be captured)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        sp_ = s.cuda_stream
+        call("zk_graph_begin", sp_)
+        try:
+            self._decode_step(ws, B, st, sp, sp_)
+        finally:
+            g = _lib.P()
+            call("zk_graph_end", sp_, C.byref(g))
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        ws["graph"] = g.value
+        ws["_keep"] = (st, sp)
+        return g.value
+
+
+import ctypes as C  # noqa: E402
+
+
+def C_ref(x):
+    return C.byref(x)
+
+
+def finalize(delayed: torch.Tensor, offset: int, P: int, stream) -> list:
+    """Output trim (model.py:437-457), on the device."""
+    B, K, Ld = delayed.shape
+    out = torch.empty(B, K, Ld - K, dtype=torch.int64, device=delayed.device)
+    call("zk_delay_revert", ptr(delayed), B, K, Ld, ptr(out), stream)
+    eos_pos = (out[:, 0, :] == EOS).int().argmax(dim=-1)
+    eos_pos[eos_pos == 0] = out.shape[2]
+    out = out[..., : offset - 9]
+    out.masked_fill_(out >= 1024, 0)
+    eos_pos = eos_pos.tolist()
+    return [out[i, :, P:eos_pos[i]].clone() for i in range(out.shape[0])]

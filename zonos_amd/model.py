@@ -1,0 +1,97 @@
+"""Zonos model API mirror (zonos/model.py:22-457) backed by the HIP engine.
+
+Kept from the reference: ``Zonos.from_pretrained`` / ``from_local`` / ``generate`` /
+``autoencoder`` / ``embed_codes`` semantics and the same safetensors key names
+(backbone.layers.{i}.{norm,mixer.in_proj,mixer.out_proj,norm2,mlp.fc1,mlp.fc2},
+backbone.norm_f, embeddings.{k}, heads.{k}). The text/speaker front end
+(prepare_conditioning, make_speaker_embedding) is outside this engine's scope: callers
+pass the [2B, Lc, D] prefix conditioning produced by the reference's PrefixConditioner.
+"""
+from __future__ import annotations
+
+import json
+from typing import Callable
+
+import torch
+
+from .autoencoder import DACAutoencoder
+from .config import ZonosConfig
+from .engine import EngineConfig, HipDecoder
+from .utils import DEFAULT_DEVICE, hub_download
+
+
+class Zonos:
+    def __init__(self, config: ZonosConfig, state_dict: dict, device=DEFAULT_DEVICE,
+                 autoencoder: DACAutoencoder | None = None):
+        if config.backbone.ssm_cfg:
+            raise NotImplementedError("the hybrid (Mamba2) backbone is not implemented by the HIP engine yet")
+        self.config = config
+        self.eos_token_id = config.eos_token_id
+        self.masked_token_id = config.masked_token_id
+        self.device = torch.device(device)
+        self.engine = HipDecoder(EngineConfig.from_backbone_config(config.backbone), state_dict, self.device)
+        self._autoencoder = autoencoder
+
+    @property
+    def autoencoder(self) -> DACAutoencoder:
+        if self._autoencoder is None:
+            self._autoencoder = DACAutoencoder(device=self.device)
+        return self._autoencoder
+
+    @autoencoder.setter
+    def autoencoder(self, ae):
+        self._autoencoder = ae
+
+    @classmethod
+    def from_pretrained(cls, repo_id: str, revision: str | None = None, device=DEFAULT_DEVICE, **kwargs) -> "Zonos":
+        config_path = hub_download(repo_id=repo_id, filename="config.json", revision=revision)
+        model_path = hub_download(repo_id=repo_id, filename="model.safetensors", revision=revision)
+        return cls.from_local(config_path, model_path, device, **kwargs)
+
+    @classmethod
+    def from_local(cls, config_path: str, model_path: str, device=DEFAULT_DEVICE, backbone: str | None = None,
+                   autoencoder: DACAutoencoder | None = None) -> "Zonos":
+        from safetensors import safe_open
+        config = ZonosConfig.from_dict(json.load(open(config_path)))
+        sd = {}
+        with safe_open(model_path, framework="pt") as f:
+            for k in f.keys():
+                if k.startswith(("backbone.", "embeddings.", "heads.")):
+                    sd[k] = f.get_tensor(k)
+        return cls(config, sd, device, autoencoder)
+
+    def prepare_conditioning(self, cond_dict: dict, uncond_dict: dict | None = None) -> torch.Tensor:
+        raise NotImplementedError("PrefixConditioner (zonos/conditioning.py) is outside the HIP engine's scope; "
+                                  "pass the [2B, Lc, d_model] prefix conditioning to generate()")
+
+    def make_speaker_embedding(self, wav, sr):
+        raise NotImplementedError("speaker embedding (zonos/speaker_cloning.py) is outside the HIP engine's scope")
+
+    @torch.inference_mode()
+    def generate(self, prefix_conditioning: torch.Tensor, audio_prefix_codes: torch.Tensor | None = None,
+                 max_new_tokens: int = 86 * 30, cfg_scale: float = 2.0, batch_size: int = 1,
+                 sampling_params: dict = dict(top_p=0, top_k=0, min_p=0, linear=0.55, conf=0.4, quad=0.0,
+                                              repetition_penalty=3.0, repetition_penalty_window=2, temperature=1.0),
+                 progress_bar: bool = True, disable_torch_compile: bool = False,
+                 callback: Callable[[torch.Tensor, int, int], bool] | None = None, *, seed: int | None = None,
+                 row_base: int = 0, force_full_length: bool = False):
+        """model.py:224-457. ``disable_torch_compile`` is accepted and ignored (the step is a
+        captured hipGraph). ``seed`` keys the sampling noise; by default it is drawn from
+        torch's global generator so ``torch.manual_seed`` makes runs reproducible."""
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        prog = None
+        if progress_bar:
+            try:
+                from tqdm import tqdm
+                Ld = (0 if audio_prefix_codes is None else audio_prefix_codes.shape[2]) + max_new_tokens + 9
+                prog = tqdm(total=Ld - 1 - (0 if audio_prefix_codes is None else audio_prefix_codes.shape[2]),
+                            desc="Generating")
+            except ImportError:
+                prog = None
+        out = self.engine.generate(prefix_conditioning.to(self.device), audio_prefix_codes, max_new_tokens,
+                                   cfg_scale, batch_size, sampling_params, seed=seed, row_base=row_base,
+                                   force_full_length=force_full_length, callback=callback, progress=prog)
+        if prog is not None:
+            prog.close()
+        return out
