@@ -258,9 +258,11 @@ def shape_probs(probs, top_p=0.0, top_k=0, min_p=0.0, linear=0.0, conf=0.0, quad
 
 
 def sample(logits, noise=None, temperature=1.0, top_p=0.0, top_k=0, min_p=0.0, linear=0.0, conf=0.0,
-           quad=0.0, generated_tokens=None, repetition_penalty=3.0, repetition_penalty_window=2, **_):
+           quad=0.0, generated_tokens=None, repetition_penalty=3.0, repetition_penalty_window=2,
+           decision: list | None = None, **_):
     """sample_from_logits (sampling.py:232-328) with the Exp(1) race noise passed in explicitly
-    (the reference draws it from torch's generator in multinomial, sampling.py:26-28)."""
+    (the reference draws it from torch's generator in multinomial, sampling.py:26-28).
+    ``decision`` (test instrumentation) receives the array whose argmax is the token."""
     if not isinstance(repetition_penalty, torch.Tensor):
         repetition_penalty = torch.tensor(repetition_penalty, dtype=logits.dtype)
     if (repetition_penalty != 1.0).any() and generated_tokens is not None:
@@ -268,7 +270,11 @@ def sample(logits, noise=None, temperature=1.0, top_p=0.0, top_k=0, min_p=0.0, l
     if temperature > 0:
         probs = torch.softmax(logits / temperature, dim=-1)
         probs = shape_probs(probs, top_p, top_k, min_p, linear, conf, quad)
+        if decision is not None:
+            decision.append(("ratio", probs / noise))
         return torch.argmax(probs / noise, dim=-1, keepdim=True).to(torch.int64)
+    if decision is not None:
+        decision.append(("logit", logits.clone()))
     return torch.argmax(logits, dim=-1, keepdim=True)
 
 
@@ -302,7 +308,8 @@ DEFAULT_SAMPLING = dict(top_p=0, top_k=0, min_p=0, linear=0.55, conf=0.4, quad=0
 def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefix_codes=None,
              max_new_tokens: int = 86 * 30, cfg_scale: float = 2.0, batch_size: int = 1,
              sampling_params: dict = DEFAULT_SAMPLING, seed: int = 0, row_base: int = 0,
-             trace: dict | None = None, force_full_length: bool = False, max_steps_run: int | None = None):
+             trace: dict | None = None, force_full_length: bool = False, max_steps_run: int | None = None,
+             force_delayed: torch.Tensor | None = None):
     """Restatement of Zonos.generate (model.py:224-457) on CPU.
 
     Noise for sampler call (step, draw) comes from oracle.philox.exp_noise(seed, step, draw, ...):
@@ -310,6 +317,8 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
     resample (model.py:388). ``force_full_length`` adds -inf to the cb0 EOS logit so every row
     runs max_steps (the benchmark mode). ``max_steps_run`` stops the loop early
     (CPU baseline windows). ``trace`` (optional dict) receives per-step logits/tokens.
+    ``force_delayed`` (test instrumentation) overwrites every written frame with the given
+    delayed codes after it is sampled (teacher forcing on a recorded history).
     """
     assert cfg_scale != 1, "TODO: add support for cfg_scale=1"   # model.py:247
     if batch_size * 2 != prefix_conditioning.shape[0]:
@@ -334,13 +343,17 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
     logits = compute_logits(W, cfg, h, kv, freqs, cfg_scale)
     if force_full_length:
         logits[:, 0, EOS] = -torch.inf
-    tok = sample(logits, noise(0, 0), **sp)
+    dec = [] if trace is not None else None
+    tok = sample(logits, noise(0, 0), decision=dec, **sp)
     if trace is not None:
+        trace.setdefault("decision", []).append(dec)
         trace.setdefault("logits", []).append(logits.clone())
         trace.setdefault("tokens", []).append(tok.clone())
     offset = P + 1
     frame = delayed[..., offset:offset + 1]
     delayed[..., offset:offset + 1] = torch.where(frame == UNKNOWN, tok, frame)
+    if force_delayed is not None:
+        delayed[..., offset:offset + 1] = force_delayed[..., offset:offset + 1]
     kv.seqlen_offset += Lc + P + 1
     kv.lengths[:] += Lc + P + 1
 
@@ -370,14 +383,15 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
         logits[act, 0, EOS] = -torch.inf
         steps_after[act] -= 1
         gen = delayed[..., :offset]
-        tok = sample(logits, noise(step, 0), generated_tokens=gen, **sp)
+        dec = [] if trace is not None else None
+        tok = sample(logits, noise(step, 0), generated_tokens=gen, decision=dec, **sp)
         eos0 = tok[:, 0] == EOS
         new = eos0[:, 0] & (~eos_mode)
         if new.any():
             eos_mode[new] = True
             steps_after[new] = 6
             logits[new, 0, EOS] = -torch.inf
-            tok = sample(logits, noise(step, 1), generated_tokens=gen, **sp)
+            tok = sample(logits, noise(step, 1), generated_tokens=gen, decision=dec, **sp)
             eos0 = tok[:, 0] == EOS
         remaining[eos0[:, 0]] = torch.minimum(remaining[eos0[:, 0]], torch.tensor(9))
         stopping |= eos0[:, 0]
@@ -389,8 +403,11 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
                 tok[i, j] = EOS
         frame = delayed[..., offset:offset + 1]
         delayed[..., offset:offset + 1] = torch.where(frame == UNKNOWN, tok, frame)
+        if force_delayed is not None:
+            delayed[..., offset:offset + 1] = force_delayed[..., offset:offset + 1]
         if trace is not None:
             trace["tokens"].append(tok.clone())
+            trace["decision"].append(dec)
         kv.seqlen_offset += 1
         kv.lengths[:] += 1
         remaining -= 1

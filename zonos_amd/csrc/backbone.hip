@@ -44,6 +44,7 @@ ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, 
             for (int e = 0; e < 8; ++e) { const float d = x[j * 8 + e] - mean; v += d * d; }
     const float var = block_sum<NT>(v, red) / (float)D;
     const float rstd = 1.0f / sqrtf(var + eps);
+    const float nb = -rstd * mean;
 #pragma unroll
     for (int j = 0; j < n8; ++j) {
         const int c = (threadIdx.x + NT * j) * 8;
@@ -52,7 +53,8 @@ ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, 
         unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
         unpack8(*reinterpret_cast<const uint4*>(b + c), bf);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (x[j * 8 + e] - mean) * rstd * wf[e] + bf[e];
+        for (int e = 0; e < 8; ++e)
+            o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(x[j * 8 + e], rstd), nb), wf[e]), bf[e]);
         *reinterpret_cast<uint4*>(y + c) = pack8(o);
     }
 }
@@ -362,39 +364,42 @@ __global__ __launch_bounds__(256) void k_attn_prefill(const bf16_t* q, const bf1
     __syncthreads();
     const bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
     const bf16_t* vb = vrows + ((size_t)r * Hkv + g) * S * HD;
-    float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
+    // Two passes like the CPU flash kernel on a single KV block: exact row max first, then
+    // p = exp(s - max) summed in fp32 and rounded to bf16 for the P.V product.
+    auto score = [&](int key) -> float {
+        float acc = 0.f;
+        const uint4* kr = reinterpret_cast<const uint4*>(kb + (size_t)key * HD);
+#pragma unroll
+        for (int i = 0; i < HD / 8; ++i) {
+            float a[8], bq[8];
+            unpack8(kr[i], a);
+            unpack8(sq[w][i], bq);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc += a[e] * bq[e];
+        }
+        return acc * scale;
+    };
+    float m = -INFINITY;
     for (int c0 = 0; c0 <= t; c0 += 64) {
         const int key = c0 + lane;
-        float sv = -INFINITY;
-        if (key <= t) {
-            float acc = 0.f;
-            const uint4* kr = reinterpret_cast<const uint4*>(kb + (size_t)key * HD);
-#pragma unroll
-            for (int i = 0; i < HD / 8; ++i) {
-                float a[8], bq[8];
-                unpack8(kr[i], a);
-                unpack8(sq[w][i], bq);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc += a[e] * bq[e];
-            }
-            sv = acc * scale;
-        }
-        const float cm = wave_max(sv);
-        const float mn = fmaxf(m, cm);
-        const float corr = (m == -INFINITY) ? 0.f : __expf(m - mn);
-        const float p = (sv == -INFINITY) ? 0.f : __expf(sv - mn);
-        l = l * corr + wave_sum(p);
-        o0 *= corr;
-        o1 *= corr;
+        if (key <= t) m = fmaxf(m, score(key));
+    }
+    m = wave_max(m);
+    float l = 0.f, o0 = 0.f, o1 = 0.f;
+    for (int c0 = 0; c0 <= t; c0 += 64) {
+        const int key = c0 + lane;
+        const float p = (key <= t) ? __expf(score(key) - m) : 0.f;
+        l += p;
+        const float pb = round_bf(p);
         const int nk = min(64, t + 1 - c0);
         for (int j = 0; j < nk; ++j) {
-            const float pj = __shfl(p, j, 64);
+            const float pj = __shfl(pb, j, 64);
             const uint32_t vv = *reinterpret_cast<const uint32_t*>(vb + (size_t)(c0 + j) * HD + 2 * lane);
             o0 += pj * __uint_as_float(vv << 16);
             o1 += pj * __uint_as_float(vv & 0xffff0000u);
         }
-        m = mn;
     }
+    l = wave_sum(l);
     if (active) {
         const float inv = 1.0f / l;
         *reinterpret_cast<uint32_t*>(out + ((size_t)(r * S + t) * H + h) * HD + 2 * lane) = pack2(o0 * inv, o1 * inv);

@@ -384,8 +384,10 @@ __global__ __launch_bounds__(NT) void k_eos_step(zk_gen_state st, int prefill, i
         for (int k = 0; k < K; ++k) {
             int v = tok[k];
             if (stop) v = k < idx ? MASK : (k == idx ? EOS : v);           // model.py:410-414
-            int64_t* d = st.delayed + ((size_t)b * K + k) * Ld + offset;
-            if (*d == -1) *d = v;                                          // model.py:417-418
+            if (offset < Ld) {   // the reference's last iteration writes an empty slice
+                int64_t* d = st.delayed + ((size_t)b * K + k) * Ld + offset;
+                if (*d == -1) *d = v;                                      // model.py:417-418
+            }
         }
         rem -= 1;                                                          // model.py:424
         st.remaining[b] = rem;
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(NT) void k_eos_step(zk_gen_state st, int prefill, i
         scal[0] = offset + 1;
         scal[1] += 1;
         scal[2] += 1;
-        if (s_max <= 0 || offset + 1 >= Ld) scal[3] = 1;
+        if (s_max <= 0 || offset >= Ld) scal[3] = 1;
         if (any) scal[4] += 1;
     }
 }

@@ -240,7 +240,8 @@ class HipDecoder:
     def generate(self, prefix_conditioning: torch.Tensor, audio_prefix_codes=None, max_new_tokens: int = 86 * 30,
                  cfg_scale: float = 2.0, batch_size: int = 1, sampling_params: dict | None = None,
                  seed: int = 0, row_base: int = 0, force_full_length: bool = False, callback=None,
-                 progress=None, poll_every: int = 16, trace: dict | None = None, use_graph: bool = True):
+                 progress=None, poll_every: int = 16, trace: dict | None = None, use_graph: bool = True,
+                 _after_prefill=None):
         """Zonos.generate (model.py:224-457). Returns the list of int64 [9, T_i] code tensors.
 
         ``trace`` (optional dict) receives per-step fp32 CFG logits (before bias) and the
@@ -286,6 +287,8 @@ class HipDecoder:
         call("zk_sample_heads", ptr(ws["part"]), ws["splits"]["heads"], C_ref(st), C_ref(sp), 1, 0, ptr(ws["dbg"]),
              stream)
         call("zk_eos_step", C_ref(st), 1, P + 1, stream)
+        if _after_prefill is not None:      # test hook (teacher forcing of the first frame)
+            _after_prefill(ws["delayed"][..., P + 1:P + 2])
         if trace is not None:
             trace.setdefault("logits", []).append(ws["dbg"].clone())
             trace.setdefault("tokens", []).append(ws["tok0"].view(B, N_CB, 1).long().clone())
@@ -336,6 +339,10 @@ class HipDecoder:
             trace["delayed"] = ws["delayed"].clone()
             trace["offset"] = offset
         return finalize(ws["delayed"], offset, P, stream)
+
+    def last_logits(self) -> torch.Tensor:
+        """fp32 CFG logits (before bias) of the last executed step [B][9][1026] (test hook)."""
+        return self._ws["dbg"]
 
     def _capture(self, ws, B, st, sp, stream):
         if ws.get("graph"):
