@@ -1,0 +1,233 @@
+"""Benchmark: DAC codes/s + real-time factor of the Zonos hot path on MI355X.
+
+Workload (BASELINE.json configs[2]): Zonos-v0.1-transformer
+(D=2048, 26 layers, 16/4 heads, FFN 8192, 1.62 B params, seeded random bf16 weights --
+no checkpoint is available offline), batch 64 utterances per GPU, synthetic LayerNorm'd
+conditioning Lc=400, 10 prefix frames, 2580 new tokens (30 s of audio) with EOS
+acceptance disabled so every row runs the full length, CLI sampling defaults; then the
+DAC decoder (descript/dac_44khz geometry, seeded fp32 weights) turns all codes into
+waveforms. One "step" = generate() + DAC decode of the whole per-GPU batch.
+
+Multi-GPU: one process per GPU (torchrun), utterances sharded by rank (row_base keys the
+noise, so codes equal a single big batch), RCCL all_gather of the int16 codes at the end
+of each step; value = codes of all ranks / max-over-ranks wall time ("scaling": "weak").
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+FRAME_RATE = 44100 / 512          # DAC frames per second of audio (86.13)
+HBM_PEAK_GBS = 8000.0             # MI355X spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)))
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--lc", type=int, default=400)
+    ap.add_argument("--prefix", type=int, default=10)
+    ap.add_argument("--new-tokens", type=int, default=2580)
+    ap.add_argument("--layers", type=int, default=26)
+    ap.add_argument("--no-dac", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def attn_roofline(eng, ctx, reps=50):
+    """Time the dominant kernel (split-KV decode attention) with HIP events on its stream at
+    the workload's mean context; algorithmic bytes = K+V rows read + q read + out write."""
+    import ctypes as C
+
+    from zonos_amd import _lib
+    from zonos_amd._lib import call, ptr
+    ws = eng._ws
+    c = eng.cfg
+    R, Hk, hd, H = ws["R"], c.n_kv, c.head_dim, c.n_heads
+    kc, vt = eng._kv(ws, c.n_layer // 2)
+    stream = _lib.stream_ptr()
+    e0, e1 = _lib.P(), _lib.P()
+    call("zk_event_create", C.byref(e0))
+    call("zk_event_create", C.byref(e1))
+    args = (ptr(ws["q"]), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], ctx, None, ptr(ws["attn_work"]),
+            ws["max_splits"], ptr(ws["y"]), None, stream)
+    for _ in range(5):
+        call("zk_attn_decode", *args)
+    call("zk_event_record", e0.value, stream)
+    for _ in range(reps):
+        call("zk_attn_decode", *args)
+    call("zk_event_record", e1.value, stream)
+    ms = C.c_float()
+    call("zk_event_elapsed_ms", e0.value, e1.value, C.byref(ms))
+    call("zk_event_destroy", e0.value)
+    call("zk_event_destroy", e1.value)
+    per_launch_s = ms.value / 1e3 / reps
+    bytes_per_launch = R * ctx * Hk * hd * 2 * 2 + R * H * hd * 2 * 2
+    ach = bytes_per_launch / per_launch_s / 1e9
+    return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
+                traffic=None, kernel="k_attn_decode+k_attn_combine", ctx=ctx,
+                bytes_per_launch=bytes_per_launch, us_per_launch=round(per_launch_s * 1e6, 2))
+
+
+def cpu_baseline(args):
+    """Oracle (CPU restatement, validated against the reference) timed on this host: decode
+    steps at B=64 at 3 context lengths (KV cache pre-filled) + a 43-frame DAC decode; scaled
+    to codes/s of the same workload (prefill excluded, <1% of the GPU time)."""
+    from oracle import dac_ref, zonos_ref
+    cores = os.cpu_count() or 1
+    threads = min(cores, 64)
+    torch.set_num_threads(threads)
+    cfg = zonos_ref.ZONOS_V01_TRANSFORMER
+    W = zonos_ref.pad_heads(zonos_ref.make_weights(cfg, seed=0), cfg)
+    B = args.batch
+    N = args.new_tokens + 8
+    ctx0 = args.lc + args.prefix + 1
+    freqs = zonos_ref.rope_table(16384, cfg.head_dim)
+    times = []
+    t_begin = time.time()
+    for frac in (0.1, 0.5, 0.9):
+        ctx = int(ctx0 + frac * N)
+        kv = zonos_ref.KVCache(cfg, 2 * B, ctx + 1)
+        for layer in kv.kv:
+            layer.normal_()
+        kv.seqlen_offset = ctx
+        kv.lengths[:] = ctx
+        ids = torch.randint(0, 1024, (2 * B, 9, 1))
+        for _ in range(args.cpu_sample_steps):
+            t = time.time()
+            with torch.no_grad():
+                zonos_ref.compute_logits(W, cfg, zonos_ref.embed_codes(W, cfg, ids), kv, freqs, 2.0)
+            times.append(time.time() - t)
+            kv.seqlen_offset = ctx
+            kv.lengths[:] = ctx
+    step_s = sum(times) / len(times)
+    dW = dac_ref.make_dac_weights(dac_ref.DAC_44KHZ, seed=0)
+    T = 43
+    codes = torch.randint(0, 1024, (1, 9, T))
+    t = time.time()
+    dac_ref.decode(dW, dac_ref.DAC_44KHZ, codes)
+    dac_s_per_frame = (time.time() - t) / T
+    total_s = N * step_s + B * args.new_tokens * dac_s_per_frame
+    codes_total = B * args.new_tokens * 9
+    return dict(value=round(codes_total / total_s, 2), unit="codes/s", cores=threads, kind="port",
+                sample=f"oracle decode step B={B} at ctx {ctx0 + int(0.1 * N)}/{ctx0 + int(0.5 * N)}/"
+                       f"{ctx0 + int(0.9 * N)} x{args.cpu_sample_steps} (mean {step_s:.3f} s/step) + DAC 43 frames "
+                       f"({dac_s_per_frame * 1e3:.1f} ms/frame); scaled to {N} steps + {B * args.new_tokens} frames; "
+                       f"{time.time() - t_begin:.1f} s of CPU work",
+                step_s=round(step_s, 4), dac_ms_per_frame=round(dac_s_per_frame * 1e3, 2))
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from zonos_amd import synthetic
+    from zonos_amd.autoencoder import DacSpec, HipDacDecoder
+    from zonos_amd.engine import EngineConfig, HipDecoder
+
+    mc = dict(synthetic.ZONOS_V01, n_layer=args.layers)
+    W = synthetic.backbone_weights(dev, seed=0, **mc)
+    eng = HipDecoder(EngineConfig(**mc), W, dev)
+    del W
+    dac = None if args.no_dac else HipDacDecoder(DacSpec(), synthetic.dac_weights(dev), dev)
+    B = args.batch
+    cond = synthetic.conditioning(B, args.lc, mc["d_model"], seed=1 + rank, device=dev)
+    prefix = synthetic.prefix_codes(B, args.prefix, seed=3 + rank, device=dev) if args.prefix else None
+    sp = dict(top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
+              repetition_penalty_window=8, temperature=1.0)
+    stats = {"gen_s": 0.0, "dac_s": 0.0}
+
+    def step(i, timed):
+        t0 = time.time()
+        codes = eng.generate(cond, prefix, args.new_tokens, 2.0, B, sp, seed=1000 + i, row_base=rank * B,
+                             force_full_length=True, poll_every=64)
+        torch.cuda.synchronize(dev)
+        t1 = time.time()
+        if dac is not None:
+            dac.decode_list(codes)
+        torch.cuda.synchronize(dev)
+        t2 = time.time()
+        if dist is not None:
+            local_codes = torch.stack(codes).to(torch.int16)
+            gathered = [torch.empty_like(local_codes) for _ in range(world)]
+            dist.all_gather(gathered, local_codes)
+        if timed:
+            stats["gen_s"] += t1 - t0
+            stats["dac_s"] += t2 - t1
+        return sum(int(c.shape[1]) for c in codes)
+
+    for i in range(args.warmup):
+        step(i, False)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.time()
+    frames = 0
+    for i in range(args.steps):
+        frames += step(args.warmup + i, True)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.time() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        fr = torch.tensor([frames], device=dev, dtype=torch.float64)
+        dist.all_reduce(fr)
+        frames = int(fr.item())
+
+    if rank == 0:
+        codes_s = frames * 9 / elapsed
+        audio_s = frames / FRAME_RATE
+        ctx_mean = args.lc + args.prefix + 1 + (args.new_tokens + 8) // 2
+        roof = attn_roofline(eng, ctx_mean)
+        out = {
+            "metric": "DAC codes/sec (end-to-end generate + DAC decode), Zonos-v0.1-transformer batch=64/GPU",
+            "value": round(codes_s, 1), "unit": "codes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded random weights + LayerNorm'd random conditioning; no checkpoint offline)",
+            "config": {"workload": "c3: B=64/GPU, Lc=400, prefix 10, 2580 new tokens (30 s), EOS disabled, "
+                                   "CLI sampling (linear .65 conf .4 rep 2.5/8), DAC decode of all codes",
+                       "model": "Zonos-v0.1-transformer", "global_batch": B * world,
+                       "seq_len": args.lc + args.prefix + args.new_tokens + 9, "parallelism": f"dp{world}"},
+            "rtf": round(audio_s / elapsed, 2),
+            "breakdown": {"generate_s_per_step": round(stats["gen_s"] / args.steps, 3),
+                          "dac_s_per_step": round(stats["dac_s"] / args.steps, 3),
+                          "generate_codes_s": round(frames / world * 9 / max(stats["gen_s"], 1e-9) * world, 1),
+                          "decode_ms_per_token_step": round(stats["gen_s"] / args.steps / (args.new_tokens + 8) * 1e3,
+                                                            3)},
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
