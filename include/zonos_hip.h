@@ -185,6 +185,22 @@ int zk_dac_conv(const float* in, int B, int Cin, int Tin, const float* alpha,
  * [s][Cout][Cin][2] so that zk_dac_conv(ks=2, pad=1, out_stride=s, out_off=r-ceil(s/2)). */
 int zk_dac_prep_convt(const float* w, int Cin, int Cout, int s, float* w_out, void* stream);
 
+/* fp16-MFMA variant of zk_dac_conv (same semantics). npass = 3: split precision
+ * (hi/lo fp16 operands, hi*hi + lo*hi + hi*lo, ~fp32 accuracy); npass = 1: plain fp16
+ * operands (the reference's own GPU numerics: autocast fp16, autoencoder.py:46).
+ * Weights prepacked by zk_dac_prep_w16: mode 0 conv [Cout][Cin][ks] -> [ks][Cout][Cin];
+ * mode 1 ConvTranspose1d [Cin][Cout][2s] -> [s][2][Cout][Cin] (phase r at offset 2*r*Cout*Cin,
+ * run with ks=2, dil=1, pad=1, out_stride=s, out_off=r-ceil(s/2)). Cin % 32 == 0. */
+int zk_dac_prep_w16(const float* w, int Cout, int Cin, int ks, int s, int mode, uint16_t* w_hi,
+                    uint16_t* w_lo, void* stream);
+int zk_dac_conv16(const float* in, int B, int Cin, int Tin, const float* alpha, const uint16_t* w_hi,
+                  const uint16_t* w_lo, const float* bias, int Cout, int ks, int dil, int pad,
+                  int Qn, int out_stride, int out_off, float* out, int Tout, const float* resid,
+                  int do_tanh, const int32_t* lens, int in_scale, int out_scale, int npass, void* stream);
+/* Final Snake -> Conv1d(C -> 1, k7, pad 3) -> tanh (modeling_dac.py:437-439); out [B][T]. */
+int zk_dac_tail(const float* in, int B, int C, int T, const float* alpha, const float* w,
+                const float* bias, float* out, const int32_t* lens, int scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,25 +13,30 @@ pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def _dec(name):
+def _dec(name, precision="fp16x3"):
     from zonos_amd.autoencoder import DacSpec, HipDacDecoder
     d = np.load(os.path.join(G, f"{name}.npz"))
     c = TINY_DAC if name == "dac_tiny" else dac_ref.DAC_44KHZ
     W = dac_ref.make_dac_weights(c, seed=int(d["seed"]))
     spec = DacSpec(c.hidden_size, c.decoder_hidden_size, c.upsampling_ratios)
-    return HipDacDecoder(spec, W, "cuda"), d, c, W
+    return HipDacDecoder(spec, W, "cuda", precision=precision), d, c, W
 
 
-@pytest.mark.parametrize("name", ["dac_tiny", "dac_44k"])
-def test_dac_decode_golden(name):
-    dec, d, c, W = _dec(name)
+@pytest.mark.parametrize("name,precision", [("dac_tiny", "fp16x3"), ("dac_44k", "fp16x3"), ("dac_44k", "fp32"),
+                                            ("dac_44k", "fp16")])
+def test_dac_decode_golden(name, precision):
+    """fp16x3 (default) and fp32 are ~fp32-exact; fp16 = the reference's GPU autocast numerics
+    (measured on CPU emulation: RMS 6.3e-5 on this fixture) -- all within the 1e-4 bar."""
+    dec, d, c, W = _dec(name, precision)
     codes = torch.from_numpy(d["codes"].astype(np.int64)).cuda()
     wav = dec.decode_padded(codes).cpu()
     ref = torch.from_numpy(d["wav"])
     assert wav.shape == ref.shape
     rms = (wav - ref).pow(2).mean().sqrt().item()
     assert rms <= 1e-4, rms                       # north_star: waveform RMS error <= 1e-4 (fp32)
-    assert (wav - ref).abs().max().item() < 1e-3
+    assert (wav - ref).abs().max().item() < (2e-3 if precision == "fp16" else 1e-4)
+    if precision != "fp16":
+        assert rms <= 1e-5, rms
 
 
 @pytest.mark.parametrize("name", ["dac_tiny", "dac_44k"])

@@ -1,0 +1,101 @@
+"""Per-kernel timing at the decode-step shapes of Zonos-v0.1 (B=64 -> 128 rows), HIP events.
+    python tools/microbench.py [gemm|attn|dac|all]"""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from zonos_amd import _lib  # noqa: E402
+from zonos_amd._lib import call, ptr  # noqa: E402
+from zonos_amd.engine import _split_for  # noqa: E402
+
+_lib.load()
+dev = torch.device("cuda")
+S = _lib.stream_ptr()
+
+
+def timeit(fn, reps=50, warm=5):
+    e0, e1 = _lib.P(), _lib.P()
+    call("zk_event_create", C.byref(e0))
+    call("zk_event_create", C.byref(e1))
+    for _ in range(warm):
+        fn()
+    call("zk_event_record", e0.value, S)
+    for _ in range(reps):
+        fn()
+    call("zk_event_record", e1.value, S)
+    ms = C.c_float()
+    call("zk_event_elapsed_ms", e0.value, e1.value, C.byref(ms))
+    return ms.value / reps * 1e3   # us
+
+
+def gemm():
+    M = 128
+    for name, N, K, mode in (("qkv", 3072, 2048, 0), ("o", 2048, 2048, 0), ("fc1", 16384, 2048, 1),
+                             ("fc2", 2048, 8192, 0), ("heads", 9234, 2048, 0)):
+        # distinct weight buffers per rep set so L2/MALL does not serve them: rotate 8 copies (>256 MB total)
+        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
+        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        ns = 1 if mode == 1 else _split_for(N, K, M)
+        part = torch.empty(ns * M * N, device=dev)
+        out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
+        it = [0]
+
+        def f():
+            W = Ws[it[0] % ncopy]
+            it[0] += 1
+            call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, ns, mode, ptr(part), ptr(out), None, S)
+        us = timeit(f)
+        gb = N * K * 2 / 1e9
+        print(f"gemm {name:6s} N={N:5d} K={K:5d} split={ns:2d}: {us:8.1f} us  weights {gb*1e3:6.1f} MB  "
+              f"{gb / (us * 1e-6):7.0f} GB/s", flush=True)
+        del Ws
+
+
+def attn():
+    R, H, Hk, hd = 128, 16, 4, 128
+    for ctx in (512, 1705, 2999):
+        smax = ((ctx + 255) // 256) * 256
+        ncopy = 3
+        kcs = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        vts = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        q = torch.randn(R, H * hd, device=dev).to(torch.bfloat16)
+        ms_ = smax // 256
+        work = torch.empty(R * Hk * ms_ * (8 + 4 * hd), device=dev)
+        out = torch.empty(R, H * hd, dtype=torch.bfloat16, device=dev)
+        it = [0]
+
+        def f():
+            i = it[0] % ncopy
+            it[0] += 1
+            call("zk_attn_decode", ptr(q), ptr(kcs[i]), ptr(vts[i]), R, H, Hk, hd, smax, ctx, None, ptr(work), ms_,
+                 ptr(out), None, S)
+        us = timeit(f)
+        b = R * ctx * Hk * hd * 2 * 2
+        print(f"attn ctx={ctx:5d}: {us:8.1f} us  {b/1e6:7.1f} MB  {b / (us * 1e-6) / 1e9:7.0f} GB/s", flush=True)
+
+
+def dac():
+    from zonos_amd import synthetic
+    from zonos_amd.autoencoder import DacSpec, HipDacDecoder
+    W = synthetic.dac_weights(dev)
+    for prec in ("fp32", "fp16x3", "fp16"):
+        d = HipDacDecoder(DacSpec(), W, dev, precision=prec)
+        for B, T in ((8, 256),):
+            codes = torch.randint(0, 1024, (B, 9, T), device=dev)
+            us = timeit(lambda: d.decode_padded(codes), reps=3, warm=1)
+            fl = 1.6083e9 * B * T
+            print(f"dac {prec:6s} B={B} T={T}: {us/1e3:8.1f} ms  {fl / (us * 1e-6) / 1e12:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("gemm", "all"):
+        gemm()
+    if what in ("attn", "all"):
+        attn()
+    if what in ("dac", "all"):
+        dac()

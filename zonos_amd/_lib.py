@@ -64,6 +64,9 @@ _SIGS = {
     "zk_dac_rvq_decode": [P, I, I, I, L, P, I, I, P, I, P, P],
     "zk_dac_conv": [P, I, I, I, P, P, P, I, I, I, I, I, I, I, P, I, P, I, P, I, I, P],
     "zk_dac_prep_convt": [P, I, I, I, P, P],
+    "zk_dac_prep_w16": [P, I, I, I, I, I, P, P, P],
+    "zk_dac_conv16": [P, I, I, I, P, P, P, P, I, I, I, I, I, I, I, P, I, P, I, P, I, I, I, P],
+    "zk_dac_tail": [P, I, I, I, P, P, P, P, P, I, P],
 }
 
 _lib = None

@@ -61,10 +61,16 @@ def _fold_weight_norm(sd: dict) -> dict:
 
 
 class HipDacDecoder:
-    """Decoder weights on the device (fp32) + the launch sequence of the DAC decoder."""
+    """Decoder weights on the device + the launch sequence of the DAC decoder.
 
-    def __init__(self, spec: DacSpec, state_dict: dict, device="cuda"):
+    precision: "fp16x3" (default; split-precision fp16 MFMA, ~fp32 accuracy), "fp16" (plain
+    fp16 operands = the reference's GPU autocast numerics, 3x less MFMA work) or "fp32"
+    (exact-fp32 MFMA kernel, slowest)."""
+
+    def __init__(self, spec: DacSpec, state_dict: dict, device="cuda", precision: str = "fp16x3"):
         _lib.load()
+        assert precision in ("fp16x3", "fp16", "fp32"), precision
+        self.precision = precision
         self.spec = spec
         self.device = torch.device(device)
         sd = _fold_weight_norm(state_dict)
@@ -100,10 +106,39 @@ class HipDacDecoder:
             self.blocks.append(blk)
         self.final_alpha = t("decoder.snake1.alpha").reshape(-1)
         self.conv2_w, self.conv2_b = t("decoder.conv2.weight"), t("decoder.conv2.bias")
+        if precision != "fp32":
+            self.w16 = {}
+            self._prep16("conv1", self.conv1_w, 0, stream)
+            for i, blk in enumerate(self.blocks):
+                self._prep16(f"b{i}.t", t(f"decoder.block.{i}.conv_t1.weight"), 1, stream, s=blk["stride"])
+                for j, ru in enumerate(blk["res"]):
+                    self._prep16(f"b{i}.r{j}.1", ru["w1"], 0, stream)
+                    self._prep16(f"b{i}.r{j}.2", ru["w2"], 0, stream)
         torch.cuda.synchronize(dev)
 
+    def _prep16(self, key, w, mode, stream, s=1):
+        if mode == 0:
+            cout, cin, ks = w.shape
+            n = cout * cin * ks
+        else:
+            cin, cout, k2 = w.shape
+            ks = 2
+            n = s * 2 * cout * cin
+        hi = torch.empty(n, dtype=torch.int16, device=self.device)
+        lo = torch.empty(n, dtype=torch.int16, device=self.device)
+        call("zk_dac_prep_w16", ptr(w), cout, cin, ks, s, mode, ptr(hi), ptr(lo), stream)
+        self.w16[key] = (hi, lo, cout * cin)
+
     def _conv(self, x, B, Cin, Tin, alpha, w, b, Cout, ks, dil, pad, Qn, ostride, ooff, out, Tout, resid, tanh,
-              lens, in_scale, out_scale, stream):
+              lens, in_scale, out_scale, stream, key=None, phase=0):
+        if self.precision != "fp32" and key is not None and Cin % 32 == 0:
+            hi, lo, per = self.w16[key]
+            off = phase * 2 * per * 2          # bytes: phase r of a ConvTranspose1d pack
+            npass = 3 if self.precision == "fp16x3" else 1
+            call("zk_dac_conv16", ptr(x), B, Cin, Tin, ptr(alpha), hi.data_ptr() + off, lo.data_ptr() + off, ptr(b),
+                 Cout, ks, dil, pad, Qn, ostride, ooff, ptr(out), Tout, ptr(resid), int(tanh), ptr(lens), in_scale,
+                 out_scale, npass, stream)
+            return
         call("zk_dac_conv", ptr(x), B, Cin, Tin, ptr(alpha), ptr(w), ptr(b), Cout, ks, dil, pad, Qn, ostride, ooff,
              ptr(out), Tout, ptr(resid), int(tanh), ptr(lens), in_scale, out_scale, stream)
 
@@ -125,33 +160,37 @@ class HipDacDecoder:
         C0 = self.conv1_w.shape[0]
         x = torch.empty(B, C0, T, device=dev)
         self._conv(z, B, s.hidden_size, T, None, self.conv1_w, self.conv1_b, C0, 7, 1, 3, T, 1, 0, x, T, None,
-                   False, lens, 1, 1, stream)
+                   False, lens, 1, 1, stream, key="conv1")
         del z
         L, scale = T, 1
-        for blk in self.blocks:
+        for bi, blk in enumerate(self.blocks):
             st, cin, cout = blk["stride"], blk["cin"], blk["cout"]
             Lo = L * st
             y = torch.empty(B, cout, Lo, device=dev)
             p = math.ceil(st / 2)
             for r in range(st):
                 self._conv(x, B, cin, L, blk["alpha"], blk["wt"][r], blk["bt"], cout, 2, 1, 1, L + 1, st, r - p, y,
-                           Lo, None, False, lens, scale, scale * st, stream)
+                           Lo, None, False, lens, scale, scale * st, stream, key=f"b{bi}.t", phase=r)
             del x
             scale *= st
             L = Lo
             tmp = torch.empty_like(y)
-            for ru in blk["res"]:
+            for j, ru in enumerate(blk["res"]):
                 d = ru["dil"]
                 self._conv(y, B, cout, L, ru["a1"], ru["w1"], ru["b1"], cout, 7, d, 3 * d, L, 1, 0, tmp, L, None,
-                           False, lens, scale, scale, stream)
+                           False, lens, scale, scale, stream, key=f"b{bi}.r{j}.1")
                 self._conv(tmp, B, cout, L, ru["a2"], ru["w2"], ru["b2"], cout, 1, 1, 0, L, 1, 0, y, L, y, False,
-                           lens, scale, scale, stream)
+                           lens, scale, scale, stream, key=f"b{bi}.r{j}.2")
             del tmp
             x = y
         out = torch.empty(B, 1, L, device=dev)
         cl = x.shape[1]
-        self._conv(x, B, cl, L, self.final_alpha, self.conv2_w, self.conv2_b, 1, 7, 1, 3, L, 1, 0, out, L, None,
-                   True, lens, scale, scale, stream)
+        if self.precision == "fp32":
+            self._conv(x, B, cl, L, self.final_alpha, self.conv2_w, self.conv2_b, 1, 7, 1, 3, L, 1, 0, out, L, None,
+                       True, lens, scale, scale, stream)
+        else:
+            call("zk_dac_tail", ptr(x), B, cl, L, ptr(self.final_alpha), ptr(self.conv2_w), ptr(self.conv2_b),
+                 ptr(out), ptr(lens), scale, stream)
         return out
 
     def decode_list(self, codes_list, max_batch_elems: float = 6e9) -> list:

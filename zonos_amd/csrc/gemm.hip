@@ -29,7 +29,7 @@ ZK_DEV bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 // LDS byte offset of 16-byte chunk c (0..7) of tile row `row` (128-byte rows, XOR swizzle)
 ZK_DEV int lds_off(int row, int c) { return row * 128 + ((c ^ (row & 7)) << 4); }
 
-template <int MODE>
+template <int MODE, int U>
 __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ W,
                                              int M, int N, int K, int kslice, float* __restrict__ Cpart,
                                              bf16_t* __restrict__ Cout, const int32_t* skip) {
@@ -46,66 +46,81 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
     const bool wvalid = wn < N;
     const bf16_t* wrow = W + (size_t)(wvalid ? wn : 0) * K + kbeg + lg * 8;
 
-    // activation staging: 4 chunks of 16 B per thread per K chunk
-    uint4 areg[4];
-    auto load_a = [&](int ch) {
-        const int k0 = kbeg + ch * BK;
+    // activation staging: 4 x 16 B per thread per K chunk (row = q>>3, 16-B chunk = q&7)
+    const bf16_t* arow[4];
+    int aoff[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = tid + NT * i;
-            const int row = q >> 3, c = q & 7;
-            const int m = m0 + row;
-            areg[i] = (m < M) ? *reinterpret_cast<const uint4*>(A + (size_t)m * lda + k0 + c * 8)
-                              : make_uint4(0, 0, 0, 0);
-        }
-    };
-    auto store_a = [&](int buf) {
-        char* base = smem + buf * (BM * BK * 2);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = tid + NT * i;
-            *reinterpret_cast<uint4*>(base + lds_off(q >> 3, q & 7)) = areg[i];
-        }
-    };
-    auto load_w = [&](int ch, uint4* wf) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-            wf[ks] = wvalid ? *reinterpret_cast<const uint4*>(wrow + ch * BK + ks * 32) : make_uint4(0, 0, 0, 0);
-    };
+    for (int i = 0; i < 4; ++i) {
+        const int q = tid + NT * i;
+        const int m = min(m0 + (q >> 3), M - 1);     // rows >= M compute garbage that is never stored
+        arow[i] = A + (size_t)m * lda + kbeg + (q & 7) * 8;
+        aoff[i] = lds_off(q >> 3, q & 7);
+    }
+    uint4 a0, a1, a2, a3;
+#define ZK_LOAD_A(ch)                                                         \
+    do {                                                                      \
+        const int _k = (ch) * BK;                                             \
+        a0 = *reinterpret_cast<const uint4*>(arow[0] + _k);                   \
+        a1 = *reinterpret_cast<const uint4*>(arow[1] + _k);                   \
+        a2 = *reinterpret_cast<const uint4*>(arow[2] + _k);                   \
+        a3 = *reinterpret_cast<const uint4*>(arow[3] + _k);                   \
+    } while (0)
+#define ZK_STORE_A(buf)                                                       \
+    do {                                                                      \
+        char* _b = smem + (buf) * (BM * BK * 2);                              \
+        *reinterpret_cast<uint4*>(_b + aoff[0]) = a0;                         \
+        *reinterpret_cast<uint4*>(_b + aoff[1]) = a1;                         \
+        *reinterpret_cast<uint4*>(_b + aoff[2]) = a2;                         \
+        *reinterpret_cast<uint4*>(_b + aoff[3]) = a3;                         \
+    } while (0)
 
     f32x4 acc[8];
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    uint4 wc[2], wn_[2];
-    load_a(0);
-    load_w(0, wc);
-    store_a(0);
-    __syncthreads();
-    for (int ch = 0; ch < nchunks; ++ch) {
-        const int cur = ch & 1;
-        const bool more = ch + 1 < nchunks;
-        if (more) {
-            load_a(ch + 1);
-            load_w(ch + 1, wn_);
-        }
-        const char* base = smem + cur * (BM * BK * 2);
+    // Weight stream: a register ring of U chunk slots keeps U-1 chunks (2 KB per wave each)
+    // of the once-read weights in flight while the current chunk is multiplied. Every load
+    // is unconditional (indices clamped; invalid columns stream row 0 and are never stored)
+    // so hipcc emits counted vmcnt waits, and the activation loads of the next chunk are
+    // issued BEFORE the weight prefetch so the wait that retires them (vmcnt counts in issue
+    // order) leaves the weight loads in flight. nchunks % U == 0 (host-checked).
+    constexpr int PF = U - 1;
+    uint4 wr0[U], wr1[U];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const bf16x8 b = as_frag(wc[ks]);
-#pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
-                const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
-            }
-        }
-        if (more) {
-            store_a(cur ^ 1);
-            wc[0] = wn_[0];
-            wc[1] = wn_[1];
-        }
-        __syncthreads();
+    for (int p = 0; p < PF; ++p) {
+        const int pc = min(p, nchunks - 1);
+        wr0[p] = *reinterpret_cast<const uint4*>(wrow + pc * BK);
+        wr1[p] = *reinterpret_cast<const uint4*>(wrow + pc * BK + 32);
     }
+    ZK_LOAD_A(0);
+    ZK_STORE_A(0);
+    __syncthreads();
+    for (int ch0 = 0; ch0 < nchunks; ch0 += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ch = ch0 + u;
+            ZK_LOAD_A(min(ch + 1, nchunks - 1));
+            {
+                const int pc = min(ch + PF, nchunks - 1);
+                wr0[(u + PF) % U] = *reinterpret_cast<const uint4*>(wrow + pc * BK);
+                wr1[(u + PF) % U] = *reinterpret_cast<const uint4*>(wrow + pc * BK + 32);
+            }
+            const char* base = smem + (ch & 1) * (BM * BK * 2);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const bf16x8 b = as_frag(ks == 0 ? wr0[u] : wr1[u]);
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) {
+                    const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
+                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
+                }
+            }
+            ZK_STORE_A((ch + 1) & 1);
+            __syncthreads();
+        }
+    }
+#undef ZK_LOAD_A
+#undef ZK_STORE_A
 
     // epilogue: acc[mt][i] = C[m0 + 16mt + 4lg + i][wn]
     if (MODE == 0) {
@@ -157,12 +172,17 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemm_bf16: lda=%ld", lda);
     ZK_REQUIRE(mode == 0 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_bf16: bad mode/nsplit");
     dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nsplit);
-    if (mode == 0)
-        hipLaunchKernelGGL(k_gemm<0>, grid, dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)A, lda,
-                           (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout, skip_flag);
-    else
-        hipLaunchKernelGGL(k_gemm<1>, grid, dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)A, lda,
-                           (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout, skip_flag);
+    const int nchunks = K / nsplit / BK;
+    const int U = (nchunks % 4 == 0) ? 4 : (nchunks % 2 == 0 ? 2 : 1);
+#define ZK_GEMM_LAUNCH(MODE_, U_)                                                                         \
+    hipLaunchKernelGGL((k_gemm<MODE_, U_>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)A, lda, \
+                       (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout, skip_flag)
+    if (mode == 0) {
+        if (U == 4) ZK_GEMM_LAUNCH(0, 4); else if (U == 2) ZK_GEMM_LAUNCH(0, 2); else ZK_GEMM_LAUNCH(0, 1);
+    } else {
+        if (U == 4) ZK_GEMM_LAUNCH(1, 4); else if (U == 2) ZK_GEMM_LAUNCH(1, 2); else ZK_GEMM_LAUNCH(1, 1);
+    }
+#undef ZK_GEMM_LAUNCH
     ZK_CHECK_LAUNCH("zk_gemm_bf16");
     return 0;
 }
