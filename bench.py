@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--layers", type=int, default=26)
     ap.add_argument("--no-dac", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-steps", type=int, default=2)
+    ap.add_argument("--cpu-sample-steps", type=int, default=1)
     return ap.parse_args()
 
 
@@ -64,7 +64,7 @@ def attn_roofline(eng, ctx, reps=50):
     call("zk_event_create", C.byref(e0))
     call("zk_event_create", C.byref(e1))
     args = (ptr(ws["q"]), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], ctx, None, ptr(ws["attn_work"]),
-            ws["max_splits"], ptr(ws["y"]), None, stream)
+            ws["attn_splits"], ptr(ws["y"]), None, stream)
     for _ in range(5):
         call("zk_attn_decode", *args)
     call("zk_event_record", e0.value, stream)
@@ -79,7 +79,8 @@ def attn_roofline(eng, ctx, reps=50):
     bytes_per_launch = R * ctx * Hk * hd * 2 * 2 + R * H * hd * 2 * 2
     ach = bytes_per_launch / per_launch_s / 1e9
     return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                traffic=None, kernel="k_attn_decode+k_attn_combine", ctx=ctx,
+                traffic=None, kernel="k_attn_decode" + ("+k_attn_combine" if ws["attn_splits"] > 1 else ""),
+                ctx=ctx, attn_splits=ws["attn_splits"],
                 bytes_per_launch=bytes_per_launch, us_per_launch=round(per_launch_s * 1e6, 2))
 
 
@@ -170,9 +171,8 @@ def main():
         torch.cuda.synchronize(dev)
         t2 = time.time()
         if dist is not None:
-            local_codes = torch.stack(codes).to(torch.int16)
-            gathered = [torch.empty_like(local_codes) for _ in range(world)]
-            dist.all_gather(gathered, local_codes)
+            from zonos_amd.distributed import gather_codes
+            gather_codes(codes, device=dev)
         if timed:
             stats["gen_s"] += t1 - t0
             stats["dac_s"] += t2 - t1

@@ -106,12 +106,13 @@ int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv, int
 
 /* Scaled-dot-product attention over the cache (F.scaled_dot_product_attention,
  * _torch.py:136; GQA, scale 1/sqrt(hd)).
- * decode: one query per row, keys [0, ctx) with ctx = ctx0 + *ctx_dev; split-KV over
- *         256-key chunks (work: fp32 [R][Hkv][max_splits][2G + G*hd], G <= 4).
+ * decode: one query per row, keys [0, ctx) with ctx = ctx0 + *ctx_dev; flash-decoding
+ *         over 128-key blocks split across `nsplit` workgroups per (row, kv head)
+ *         (nsplit <= Smax/128; work: fp32 [R][Hkv][nsplit][8 + 4*hd] when nsplit > 1).
  * prefill: S queries per row at positions 0..S-1, causal (is_causal=S>1), V from v_rows.
  * Output bf16 [rows][H*hd]. */
 int zk_attn_decode(const void* q, const void* k_cache, const void* vt_cache, int R, int H, int Hkv,
-                   int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int max_splits,
+                   int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int nsplit,
                    void* out, const int32_t* skip, void* stream);
 int zk_attn_prefill(const void* q, const void* k_cache, const void* v_rows, int R, int S, int H,
                     int Hkv, int hd, int Smax, void* out, void* stream);

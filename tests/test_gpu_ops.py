@@ -144,8 +144,10 @@ def _attn_setup(R, S_ctx, H, Hk, hd, smax, seed=0):
     return k, v, kc, vt
 
 
-@pytest.mark.parametrize("R,ctx,H,Hk", [(4, 1, 16, 4), (3, 300, 16, 4), (2, 1000, 2, 1), (128, 513, 16, 4)])
-def test_attention_decode(R, ctx, H, Hk):
+@pytest.mark.parametrize("R,ctx,H,Hk,nsplit", [(4, 1, 16, 4, 1), (3, 300, 16, 4, 2), (2, 1000, 2, 1, 8),
+                                                (128, 513, 16, 4, 1), (128, 1705, 16, 4, 2), (1, 2999, 16, 4, 24),
+                                                (2, 129, 16, 4, 2)])
+def test_attention_decode(R, ctx, H, Hk, nsplit):
     from zonos_amd._lib import call, ptr, stream_ptr
     hd = 128
     smax = ((ctx + 255) // 256) * 256
@@ -153,11 +155,11 @@ def test_attention_decode(R, ctx, H, Hk):
     q = torch.randn(R, 1, H, hd).to(torch.bfloat16)
     ref = F.scaled_dot_product_attention(q.transpose(1, 2).float(), k.transpose(1, 2).float(),
                                          v.transpose(1, 2).float(), enable_gqa=True).transpose(1, 2).reshape(R, H * hd)
-    max_splits = smax // 256
-    work = torch.empty(R * Hk * max_splits * (8 + 4 * hd), device=DEV)
+    nsplit = min(nsplit, smax // 128)
+    work = torch.empty(R * Hk * nsplit * (8 + 4 * hd), device=DEV)
     out = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
     qd, kd, vd = q.to(DEV), kc.to(DEV), vt.to(DEV)
-    call("zk_attn_decode", ptr(qd), ptr(kd), ptr(vd), R, H, Hk, hd, smax, ctx, None, ptr(work), max_splits, ptr(out),
+    call("zk_attn_decode", ptr(qd), ptr(kd), ptr(vd), R, H, Hk, hd, smax, ctx, None, ptr(work), nsplit, ptr(out),
          None, stream_ptr())
     # P is rounded to bf16 for the P.V MFMA (as the reference's CPU flash kernel does)
     assert (out.float().cpu() - ref).abs().max() < 2e-2

@@ -63,7 +63,13 @@ def attn():
         kcs = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
         vts = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
         q = torch.randn(R, H * hd, device=dev).to(torch.bfloat16)
-        ms_ = smax // 256
+        from zonos_amd.engine import attn_splits_for
+        for ms_ in sorted({attn_splits_for(R, Hk, smax), 1, 4}):
+            attn_one(R, H, Hk, hd, ctx, smax, kcs, vts, q, ms_, ncopy)
+
+
+def attn_one(R, H, Hk, hd, ctx, smax, kcs, vts, q, ms_, ncopy):
+    if True:
         work = torch.empty(R * Hk * ms_ * (8 + 4 * hd), device=dev)
         out = torch.empty(R, H * hd, dtype=torch.bfloat16, device=dev)
         it = [0]
@@ -75,7 +81,7 @@ def attn():
                  ptr(out), None, S)
         us = timeit(f)
         b = R * ctx * Hk * hd * 2 * 2
-        print(f"attn ctx={ctx:5d}: {us:8.1f} us  {b/1e6:7.1f} MB  {b / (us * 1e-6) / 1e9:7.0f} GB/s", flush=True)
+        print(f"attn ctx={ctx:5d} splits={ms_}: {us:8.1f} us  {b/1e6:7.1f} MB  {b / (us * 1e-6) / 1e9:7.0f} GB/s", flush=True)
 
 
 def dac():

@@ -192,150 +192,192 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit,
 }
 
 // ------------------------------------------------------------------ decode attention
-constexpr int AT_CH = 256;      // keys per workgroup (4 waves x 64)
+constexpr int AT_KB = 128;      // keys per workgroup iteration (4 waves x 32)
 constexpr int AT_G = 4;         // query heads per KV head handled by the B operand (<= 16)
+constexpr int AT_STR = 2 * AT_G + AT_G * 128;   // work floats per (r, g, split)
 
-// work layout per (r, g, split): [G] max, [G] sum, [G][hd] unnormalised output
-__global__ __launch_bounds__(256) void k_attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vt, int R,
-                                                     int H, int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
-                                                     float* work, int max_splits, float scale,
-                                                     const int32_t* skip) {
+// One 32-key step of one wave: registers for K (A operand of S^T = K.Q^T) and V^T
+// (A operand of O^T = V^T.P^T). Key mapping inside the 32: MFMA row r = 4*grp + i of tile h
+// holds key 8*grp + 4*h + i, so a lane's 8 score values are the 8 CONTIGUOUS keys
+// 8*grp .. 8*grp+7 and its V^T fragment is one 16-byte load.
+struct KVFrag {
+    uint4 k[2][4];   // [tile h][d-step]
+    uint4 v[8];      // [d-tile]
+};
+
+ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int key_base, int ln, int lg) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int key = key_base + 8 * (ln >> 2) + 4 * h + (ln & 3);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            f.k[h][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)key * 128 + ks * 32 + lg * 8);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+        f.v[dt] = *reinterpret_cast<const uint4*>(vb + (size_t)(dt * 16 + ln) * Smax + key_base + 8 * lg);
+}
+
+struct AttnState {
+    float m, l;
+    f32x4 o[8];      // o[dt][i] = O^T[d = dt*16 + 4lg + i][head = ln]
+};
+
+ZK_DEV void attn_step(AttnState& st, const KVFrag& f, const bf16x8* qf, int key_base, int ctx, float scale,
+                      int lg) {
+    f32x4 sacc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        sacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(f.k[h][ks]), qf[ks], sacc[h], 0, 0, 0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int key = key_base + 8 * lg + 4 * h + i;
+            const float sv = key < ctx ? sacc[h][i] * scale : -INFINITY;
+            sacc[h][i] = sv;
+            mx = fmaxf(mx, sv);
+        }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(st.m, mx);
+    if (mn == -INFINITY) return;                       // nothing visible yet (all keys masked)
+    const float corr = (st.m == -INFINITY) ? 0.f : __expf(st.m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float pv = __expf(sacc[h][i] - mn);
+            sacc[h][i] = pv;
+            ps += pv;
+        }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    st.l = st.l * corr + ps;
+    st.m = mn;
+    const uint4 pa = make_uint4(pack2(sacc[0][0], sacc[0][1]), pack2(sacc[0][2], sacc[0][3]),
+                                pack2(sacc[1][0], sacc[1][1]), pack2(sacc[1][2], sacc[1][3]));
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st.o[dt][i] *= corr;
+        st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(f.v[dt]), as_frag(pa), st.o[dt], 0, 0, 0);
+    }
+}
+
+// Flash-decoding over the KV cache: grid (nsplit, Hkv, R); each workgroup streams its share
+// of 128-key blocks, each wave a 32-key slice of every block, with the next slice's K/V
+// loads in flight (two register sets) while the current one is multiplied; the 4 waves merge
+// (m, l, O) through LDS at the end. nsplit == 1 writes the normalised bf16 output directly.
+__global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vt, int R,
+                                                        int H, int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
+                                                        float* work, float scale, bf16_t* out, const int32_t* skip) {
     constexpr int HD = 128;
     __shared__ float s_m[4][16];
     __shared__ float s_l[4][16];
     __shared__ float s_o[4][AT_G][HD];
     if (skip && *skip) return;
-    const int split = blockIdx.x, g = blockIdx.y, r = blockIdx.z;
+    const int split = blockIdx.x, nsplit = gridDim.x, g = blockIdx.y, r = blockIdx.z;
     const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
-    const int nsplit = (ctx + AT_CH - 1) / AT_CH;
-    if (split >= nsplit) return;
+    const int nkb = (ctx + AT_KB - 1) / AT_KB;
+    const int kb0 = (int)((long)split * nkb / nsplit), kb1 = (int)((long)(split + 1) * nkb / nsplit);
     const int G = H / Hkv;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int n = lane & 15, grp = lane >> 4;
-    const int key0 = split * AT_CH + w * 64;
+    const int ln = lane & 15, lg = lane >> 4;
 
-    // Q^T fragments (B operand): B[k = d][n = head]
     bf16x8 qf[4];
     {
-        const bf16_t* qr = q + (size_t)r * H * HD + (size_t)(g * G + n) * HD;
+        const bf16_t* qr = q + (size_t)r * H * HD + (size_t)(g * G + ln) * HD;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (n < G) v = *reinterpret_cast<const uint4*>(qr + ks * 32 + grp * 8);
+            if (ln < G) v = *reinterpret_cast<const uint4*>(qr + ks * 32 + lg * 8);
             qf[ks] = as_frag(v);
         }
     }
     const bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
     const bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
 
-    // ---- S^T = K . Q^T for 64 keys (4 tiles of 16)
-    uint4 kf[4][4];
+    AttnState st;
+    st.m = -INFINITY;
+    st.l = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            kf[kt][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)(key0 + kt * 16 + n) * HD + ks * 32 + grp * 8);
-    // V^T fragments for the two 32-key steps: keys 32u + 4grp + {0..3} and 32u + 16 + 4grp + {0..3}
-    uint2 vf[2][8][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-            const bf16_t* vrow = vb + (size_t)(dt * 16 + n) * Smax + key0 + 32 * u + 4 * grp;
-            vf[u][dt][0] = *reinterpret_cast<const uint2*>(vrow);
-            vf[u][dt][1] = *reinterpret_cast<const uint2*>(vrow + 16);
-        }
-    f32x4 sacc[4];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-        sacc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            sacc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(kf[kt][ks]), qf[ks], sacc[kt], 0, 0, 0);
-    }
-    // scores: key = key0 + 16kt + 4grp + i, head = n
-    float m = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int key = key0 + kt * 16 + grp * 4 + i;
-            float sv = sacc[kt][i] * scale;
-            if (key >= ctx) sv = -INFINITY;
-            sacc[kt][i] = sv;
-            m = fmaxf(m, sv);
-        }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    if (grp == 0) s_m[w][n] = m;
-    __syncthreads();
-    const float M = fmaxf(fmaxf(s_m[0][n], s_m[1][n]), fmaxf(s_m[2][n], s_m[3][n]));
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float pv = (M == -INFINITY) ? 0.f : __expf(sacc[kt][i] - M);
-            sacc[kt][i] = pv;
-            l += pv;
-        }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    if (grp == 0) s_l[w][n] = l;
+    for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // ---- O = P . V : A = P[head][key], k-index kk=8grp+j <-> local key 32u + (j<4 ? 4grp+j : 16+4grp+j-4)
-    f32x4 oacc[8];
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const f32x4 p0 = sacc[2 * u], p1 = sacc[2 * u + 1];
-        const uint4 pa = make_uint4(pack2(p0[0], p0[1]), pack2(p0[2], p0[3]), pack2(p1[0], p1[1]),
-                                    pack2(p1[2], p1[3]));
-        // A operand needs row = head (= n), but the scores sit at column n: transpose via the
-        // MFMA: use P^T as the B operand instead and V^T as the A operand -> O^T[d][head].
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-            const uint4 va = make_uint4(vf[u][dt][0].x, vf[u][dt][0].y, vf[u][dt][1].x, vf[u][dt][1].y);
-            oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(va), as_frag(pa), oacc[dt], 0, 0, 0);
+    if (kb1 > kb0) {
+        KVFrag fa, fb;
+        const int last = kb1 - 1;
+        load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
+        for (int it = kb0; it < kb1; it += 2) {
+            load_kv(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
+            attn_step(st, fa, qf, it * AT_KB + 32 * w, ctx, scale, lg);
+            load_kv(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
+            if (it + 1 < kb1) attn_step(st, fb, qf, (it + 1) * AT_KB + 32 * w, ctx, scale, lg);
         }
     }
-    // oacc[dt][i] = O^T[d = dt*16 + 4grp + i][head = n]
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (n < AT_G) s_o[w][n][dt * 16 + grp * 4 + i] = oacc[dt][i];
+    // merge the 4 waves
+    if (lg == 0) { s_m[w][ln] = st.m; s_l[w][ln] = st.l; }
     __syncthreads();
-    // reduce the 4 waves and write the split's partial result
-    float* wp = work + (((size_t)r * Hkv + g) * max_splits + split) * (2 * AT_G + AT_G * HD);
+    const float M = fmaxf(fmaxf(s_m[0][ln], s_m[1][ln]), fmaxf(s_m[2][ln], s_m[3][ln]));
+    const float cw = (st.m == -INFINITY) ? 0.f : __expf(st.m - M);
+    if (ln < AT_G) {
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s_o[w][ln][dt * 16 + lg * 4 + i] = st.o[dt][i] * cw;
+    }
+    __syncthreads();
+    if (nsplit == 1) {
+        // normalised output for the G heads: thread -> (head, 2 channels)
+        for (int i = threadIdx.x; i < G * HD / 2; i += 256) {
+            const int h = i / (HD / 2), d = (i % (HD / 2)) * 2;
+            float Mh = -INFINITY;
+            for (int k = 0; k < 4; ++k) Mh = fmaxf(Mh, s_m[k][h]);
+            float L = 0.f;
+            for (int k = 0; k < 4; ++k) L += (s_m[k][h] == -INFINITY) ? 0.f : s_l[k][h] * __expf(s_m[k][h] - Mh);
+            const float o0 = s_o[0][h][d] + s_o[1][h][d] + s_o[2][h][d] + s_o[3][h][d];
+            const float o1 = s_o[0][h][d + 1] + s_o[1][h][d + 1] + s_o[2][h][d + 1] + s_o[3][h][d + 1];
+            const float inv = 1.0f / L;
+            *reinterpret_cast<uint32_t*>(out + (size_t)r * H * HD + (size_t)(g * G + h) * HD + d) =
+                pack2(o0 * inv, o1 * inv);
+        }
+        return;
+    }
+    float* wp = work + (((size_t)r * Hkv + g) * nsplit + split) * AT_STR;
     for (int i = threadIdx.x; i < AT_G * HD; i += 256) {
         const int h = i / HD, d = i % HD;
         wp[2 * AT_G + i] = s_o[0][h][d] + s_o[1][h][d] + s_o[2][h][d] + s_o[3][h][d];
     }
     if (threadIdx.x < AT_G) {
         const int h = threadIdx.x;
-        wp[h] = fmaxf(fmaxf(s_m[0][h], s_m[1][h]), fmaxf(s_m[2][h], s_m[3][h]));
-        wp[AT_G + h] = s_l[0][h] + s_l[1][h] + s_l[2][h] + s_l[3][h];
+        float Mh = -INFINITY;
+        for (int k = 0; k < 4; ++k) Mh = fmaxf(Mh, s_m[k][h]);
+        float L = 0.f;
+        for (int k = 0; k < 4; ++k) L += (s_m[k][h] == -INFINITY) ? 0.f : s_l[k][h] * __expf(s_m[k][h] - Mh);
+        wp[h] = Mh;
+        wp[AT_G + h] = L;
     }
 }
 
-__global__ __launch_bounds__(64) void k_attn_combine(const float* work, int H, int Hkv, int max_splits, int ctx0,
-                                                     const int32_t* ctx_dev, bf16_t* out, const int32_t* skip) {
+__global__ __launch_bounds__(64) void k_attn_combine(const float* work, int H, int Hkv, int nsplit, bf16_t* out,
+                                                     const int32_t* skip) {
     constexpr int HD = 128;
     if (skip && *skip) return;
     const int h = blockIdx.x, r = blockIdx.y;
     const int G = H / Hkv, g = h / G, j = h % G;
-    const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
-    const int nsplit = (ctx + AT_CH - 1) / AT_CH;
-    const float* base = work + ((size_t)r * Hkv + g) * max_splits * (2 * AT_G + AT_G * HD);
-    constexpr int STR = 2 * AT_G + AT_G * HD;
+    const float* base = work + ((size_t)r * Hkv + g) * nsplit * AT_STR;
     float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, base[s * STR + j]);
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, base[s * AT_STR + j]);
     float L = 0.f, o0 = 0.f, o1 = 0.f;
     const int d = threadIdx.x * 2;
     for (int s = 0; s < nsplit; ++s) {
-        const float* p = base + s * STR;
+        const float* p = base + s * AT_STR;
         const float c = (p[j] == -INFINITY) ? 0.f : __expf(p[j] - M);
         L += p[AT_G + j] * c;
         o0 += p[2 * AT_G + j * HD + d] * c;
@@ -468,20 +510,24 @@ extern "C" int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, i
 }
 
 extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt_cache, int R, int H, int Hkv,
-                              int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int max_splits,
+                              int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int nsplit,
                               void* out, const int32_t* skip, void* stream) {
     ZK_REQUIRE(hd == 128, "zk_attn_decode: head_dim %d unsupported (128 only)", hd);
     ZK_REQUIRE(H % Hkv == 0 && H / Hkv <= AT_G, "zk_attn_decode: GQA group %d > %d", H / Hkv, AT_G);
-    ZK_REQUIRE(Smax % AT_CH == 0 && max_splits * AT_CH >= Smax,
-               "zk_attn_decode: Smax=%d must be a multiple of %d covered by max_splits=%d", Smax, AT_CH, max_splits);
+    ZK_REQUIRE(Smax % AT_KB == 0, "zk_attn_decode: Smax=%d must be a multiple of %d", Smax, AT_KB);
+    ZK_REQUIRE(nsplit >= 1 && nsplit <= Smax / AT_KB, "zk_attn_decode: nsplit=%d out of [1, %d]", nsplit,
+               Smax / AT_KB);
+    ZK_REQUIRE(nsplit == 1 || work != nullptr, "zk_attn_decode: nsplit > 1 needs the work buffer");
     const float scale = 1.0f / sqrtf((float)hd);
-    hipLaunchKernelGGL(k_attn_decode, dim3(max_splits, Hkv, R), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0,
-                       ctx_dev, work, max_splits, scale, skip);
+    hipLaunchKernelGGL(k_attn_decode, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q,
+                       (const bf16_t*)k_cache, (const bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale,
+                       (bf16_t*)out, skip);
     ZK_CHECK_LAUNCH("zk_attn_decode");
-    hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, max_splits, ctx0,
-                       ctx_dev, (bf16_t*)out, skip);
-    ZK_CHECK_LAUNCH("zk_attn_combine");
+    if (nsplit > 1) {
+        hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, nsplit,
+                           (bf16_t*)out, skip);
+        ZK_CHECK_LAUNCH("zk_attn_combine");
+    }
     return 0;
 }
 

@@ -73,6 +73,13 @@ def _split_for(N: int, K: int, M: int, target_blocks: int = 256) -> int:
     return s
 
 
+def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> int:
+    """Workgroups per (row, kv head) for flash-decoding. Measured at R=128 (B=64): one
+    workgroup per (row, kv head) (512 workgroups, no combine pass) reads 5.4-5.7 TB/s at
+    ctx 1.7-3k vs 4.5-4.7 with 2 splits; small batches split the keys to fill the CUs."""
+    return max(1, min(-(-target_blocks // (R * Hkv)), smax // 128))
+
+
 class HipDecoder:
     """Owns device weights in engine layout and runs generate() on the GPU."""
 
@@ -140,15 +147,15 @@ class HipDecoder:
                       heads=_split_for(Nh, D, R))
         part_n = max(Mp * Nqkv, Mp * D, splits["qkv"] * R * Nqkv, splits["o"] * R * D, splits["fc2"] * R * D,
                      splits["heads"] * R * Nh)
-        max_splits = smax // ATTN_CHUNK
+        attn_splits = attn_splits_for(R, Hk, smax)
         ws = dict(
-            key=key, R=R, T=T, Ld=Ld, smax=smax, S_pre=S_pre, splits=splits, max_splits=max_splits,
+            key=key, R=R, T=T, Ld=Ld, smax=smax, S_pre=S_pre, splits=splits, attn_splits=attn_splits,
             kv=torch.zeros(c.n_layer, 2, R * Hk * smax * hd, dtype=bf, device=dev),
             x=torch.empty(Mp, D, dtype=bf, device=dev), xn=torch.empty(Mp, D, dtype=bf, device=dev),
             q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
             h=torch.empty(Mp, Fd, dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
             vrows=torch.empty(R * Hk * S_pre * hd, dtype=bf, device=dev),
-            attn_work=torch.empty(R * Hk * max_splits * (8 + 4 * hd), dtype=f32, device=dev),
+            attn_work=torch.empty(max(1, R * Hk * attn_splits * (8 + 4 * hd)), dtype=f32, device=dev),
             scal=torch.zeros(16, dtype=i32, device=dev),
             eos_mode=torch.zeros(B, dtype=i32, device=dev), steps_after=torch.zeros(B, dtype=i32, device=dev),
             remaining=torch.zeros(B, dtype=i32, device=dev), stopping=torch.zeros(B, dtype=i32, device=dev),
@@ -194,7 +201,7 @@ class HipDecoder:
                 call("zk_attn_prefill", ptr(q), ptr(kc), ptr(ws["vrows"]), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
             else:
                 call("zk_attn_decode", ptr(q), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1, ptr(scal[1:2]),
-                     ptr(ws["attn_work"]), ws["max_splits"], ptr(y), skip, stream)
+                     ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), skip, stream)
             call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip, stream)
             call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D, ptr(x),
                  ptr(xn), skip, stream)
