@@ -26,10 +26,18 @@ constexpr int BM = 128, BN = 64, BK = 64, NT = 256;
 
 ZK_DEV bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+// streamed-once weights: non-temporal 16-byte load (global_load_dwordx4 ... nt)
+template <bool NT_>
+ZK_DEV uint4 ldg_w(const bf16_t* p) {
+    if constexpr (NT_) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
+    else return *reinterpret_cast<const uint4*>(p);
+}
+
 // LDS byte offset of 16-byte chunk c (0..7) of tile row `row` (128-byte rows, XOR swizzle)
 ZK_DEV int lds_off(int row, int c) { return row * 128 + ((c ^ (row & 7)) << 4); }
 
-template <int MODE, int U>
+template <int MODE, int U, bool WNT = false>
 __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ W,
                                              int M, int N, int K, int kslice, float* __restrict__ Cpart,
                                              bf16_t* __restrict__ Cout, const int32_t* skip) {
@@ -89,8 +97,8 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
         const int pc = min(p, nchunks - 1);
-        wr0[p] = *reinterpret_cast<const uint4*>(wrow + pc * BK);
-        wr1[p] = *reinterpret_cast<const uint4*>(wrow + pc * BK + 32);
+        wr0[p] = ldg_w<WNT>(wrow + pc * BK);
+        wr1[p] = ldg_w<WNT>(wrow + pc * BK + 32);
     }
     ZK_LOAD_A(0);
     ZK_STORE_A(0);
@@ -102,8 +110,8 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
             ZK_LOAD_A(min(ch + 1, nchunks - 1));
             {
                 const int pc = min(ch + PF, nchunks - 1);
-                wr0[(u + PF) % U] = *reinterpret_cast<const uint4*>(wrow + pc * BK);
-                wr1[(u + PF) % U] = *reinterpret_cast<const uint4*>(wrow + pc * BK + 32);
+                wr0[(u + PF) % U] = ldg_w<WNT>(wrow + pc * BK);
+                wr1[(u + PF) % U] = ldg_w<WNT>(wrow + pc * BK + 32);
             }
             const char* base = smem + (ch & 1) * (BM * BK * 2);
 #pragma unroll
@@ -154,6 +162,129 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
     }
 }
 
+// ------------------------------------------------------------------ decode GEMM, loader-wave form
+// M <= 128. Problem with a single load queue: vmcnt retires loads in issue order, so a wave
+// that stages activations AND streams weights drains its weight prefetch every time it waits
+// for an activation chunk. Here the roles are split across waves, each with its own vmcnt
+// queue: wave 4 (the loader) moves activation chunks into an LDS ring by LDS-DMA
+// (global_load_lds_dwordx4, DA chunks ahead, XOR swizzle applied on the source address), and
+// waves 0-3 only stream weights into a PF-chunk register ring; one raw s_barrier per chunk
+// publishes the next activation chunk (it does not drain VMEM).
+constexpr int WS_NB = 6;        // LDS ring slots (16 KB each)
+constexpr int WS_DA = 4;        // activation chunks in flight (loader)
+constexpr int WS_THREADS = 320;
+constexpr int WS_PF = 4;        // weight chunks in flight per compute wave
+
+template <int MODE, int NCH, int PF>
+__global__ __launch_bounds__(WS_THREADS, 1) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
+                                                           const bf16_t* __restrict__ W, int M, int N, int K,
+                                                           int kslice, float* __restrict__ Cpart,
+                                                           bf16_t* __restrict__ Cout, const int32_t* skip) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (skip && *skip) return;
+    const int n0 = blockIdx.x * BN, split = blockIdx.z;
+    const int kbeg = split * kslice;
+    const int nchunks = kslice / BK;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int ln = lane & 15, lg = lane >> 4;
+
+    if (w == 4) {
+        // ---------------- loader wave: 16 x 1 KB LDS-DMA pieces per 16 KB chunk
+        // piece i covers tile rows 8i..8i+7; lane L lands at byte 16L of the piece:
+        // row = 8i + (L>>3), slot = L&7  ->  source 16-B chunk = slot ^ (row&7)
+        const int rl = lane >> 3, sl = lane & 7;
+        auto issue = [&](int ch) {
+            char* dst = smem + (ch % WS_NB) * (BM * BK * 2);
+            const int k0 = kbeg + ch * BK;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = 8 * i + rl;
+                const int m = min(row, M - 1);
+                const bf16_t* src = A + (size_t)m * lda + k0 + ((sl ^ (row & 7)) << 3);
+                __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 1024), 16, 0, 0);
+            }
+        };
+        const int pre = min(WS_DA, nchunks);
+        for (int c = 0; c < pre; ++c) issue(c);
+        for (int c = 0; c < nchunks; ++c) {
+            const int younger = min(c + WS_DA, nchunks) - c - 1;     // chunks issued after c
+            if (younger >= 3) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+            else if (younger == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+            else if (younger == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();                           // publish chunk c
+            asm volatile("" ::: "memory");
+            if (c + WS_DA < nchunks) issue(c + WS_DA);              // its slot was read 2 chunks ago
+        }
+        return;
+    }
+
+    // ---------------- compute waves
+    const int wn = n0 + w * 16 + ln;
+    const bool wvalid = wn < N;
+    const bf16_t* wrow = W + (size_t)(wvalid ? wn : 0) * K + kbeg + lg * 8;
+    f32x4 acc[8];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // Fully unrolled K loop (NCH chunks known at compile time): no loop back edge, so hipcc's
+    // waitcnt pass counts exactly and keeps PF chunks (2 loads each) of weights in flight
+    // (its loop-header merge otherwise drains the ring). Ring slots are compile-time indices.
+    constexpr int U = PF + 1;
+    uint4 wr0[U], wr1[U];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+        const int pc = p < NCH ? p : NCH - 1;
+        wr0[p] = ldg_w<false>(wrow + pc * BK);
+        wr1[p] = ldg_w<false>(wrow + pc * BK + 32);
+    }
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + PF < NCH) {
+            wr0[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * BK);
+            wr1[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * BK + 32);
+        }
+        __builtin_amdgcn_s_barrier();                               // chunk ch is in LDS
+        asm volatile("" ::: "memory");
+        const char* base = smem + (ch % WS_NB) * (BM * BK * 2);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt) {
+                const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
+            }
+        }
+    }
+    if (MODE == 0) {
+        float* C = Cpart + (size_t)split * M * N;
+        if (wvalid) {
+#pragma unroll
+            for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = mt * 16 + lg * 4 + i;
+                    if (m < M) C[(size_t)m * N + wn] = acc[mt][i];
+                }
+        }
+    } else {
+        const int F = N / 2;
+        const int f = (n0 + w * 16) / 2 + (ln & 7);
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float mine = round_bf(acc[mt][i]);
+                const float other = __shfl_xor(mine, 8, 64);
+                const int m = mt * 16 + lg * 4 + i;
+                if (ln < 8 && m < M && f < F) {
+                    const float sl = round_bf(other / (1.0f + expf(-other)));
+                    Cout[(size_t)m * F + f] = f2bf(mine * sl);
+                }
+            }
+    }
+}
+
 __global__ void k_permute_fc1(const bf16_t* w, int F, int D, bf16_t* out) {
     const int nr = blockIdx.x;         // new row
     const int q = nr / 16, j = nr % 16;
@@ -171,8 +302,45 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     ZK_REQUIRE(nsplit >= 1 && K % (nsplit * BK) == 0, "zk_gemm_bf16: K=%d must be a multiple of nsplit*%d", K, BK);
     ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemm_bf16: lda=%ld", lda);
     ZK_REQUIRE(mode == 0 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_bf16: bad mode/nsplit");
-    dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nsplit);
     const int nchunks = K / nsplit / BK;
+    if (M <= BM && nchunks <= 32) {
+        dim3 g((N + BN - 1) / BN, 1, nsplit);
+        const size_t lds = (size_t)WS_NB * BM * BK * 2;
+#define ZK_WS_LAUNCH(MODE_, NCH_)                                                                                  \
+    do {                                                                                                          \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, WS_PF>),                        \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                \
+        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, WS_PF>), g, dim3(WS_THREADS), lds, (hipStream_t)stream,        \
+                           (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
+                           skip_flag);                                                                             \
+        handled = true;                                                                                           \
+    } while (0)
+        bool handled = false;
+        if (mode == 0) {
+            switch (nchunks) {
+                case 2: ZK_WS_LAUNCH(0, 2); break;
+                case 4: ZK_WS_LAUNCH(0, 4); break;
+                case 8: ZK_WS_LAUNCH(0, 8); break;
+                case 16: ZK_WS_LAUNCH(0, 16); break;
+                case 32: ZK_WS_LAUNCH(0, 32); break;
+                default: break;
+            }
+        } else {
+            switch (nchunks) {
+                case 4: ZK_WS_LAUNCH(1, 4); break;
+                case 8: ZK_WS_LAUNCH(1, 8); break;
+                case 16: ZK_WS_LAUNCH(1, 16); break;
+                case 32: ZK_WS_LAUNCH(1, 32); break;
+                default: break;
+            }
+        }
+        if (handled) {
+            ZK_CHECK_LAUNCH("zk_gemm_bf16");
+            return 0;
+        }
+#undef ZK_WS_LAUNCH
+    }
+    dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nsplit);
     const int U = (nchunks % 4 == 0) ? 4 : (nchunks % 2 == 0 ? 2 : 1);
 #define ZK_GEMM_LAUNCH(MODE_, U_)                                                                         \
     hipLaunchKernelGGL((k_gemm<MODE_, U_>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)A, lda, \
