@@ -5,8 +5,10 @@ Workload (BASELINE.json configs[2]): Zonos-v0.1-transformer
 no checkpoint is available offline), batch 64 utterances per GPU, synthetic LayerNorm'd
 conditioning Lc=400, 10 prefix frames, 2580 new tokens (30 s of audio) with EOS
 acceptance disabled so every row runs the full length, CLI sampling defaults; then the
-DAC decoder (descript/dac_44khz geometry, seeded fp32 weights) turns all codes into
-waveforms. One "step" = generate() + DAC decode of the whole per-GPU batch.
+DAC decoder (descript/dac_44khz geometry, seeded fp32 weights; fp16 conv operands with fp32
+accumulation = the reference's own GPU numerics, torch.autocast fp16 at autoencoder.py:46)
+turns all codes into waveforms. One "step" = generate() + DAC decode of the whole per-GPU
+batch.
 
 Multi-GPU: one process per GPU (torchrun), utterances sharded by rank (row_base keys the
 noise, so codes equal a single big batch), RCCL all_gather of the int16 codes at the end
@@ -100,21 +102,22 @@ def cpu_baseline(args):
     freqs = zonos_ref.rope_table(16384, cfg.head_dim)
     times = []
     t_begin = time.time()
-    for frac in (0.1, 0.5, 0.9):
-        ctx = int(ctx0 + frac * N)
-        kv = zonos_ref.KVCache(cfg, 2 * B, ctx + 1)
-        for layer in kv.kv:
-            layer.normal_()
-        kv.seqlen_offset = ctx
-        kv.lengths[:] = ctx
+    ctxs = [int(ctx0 + frac * N) for frac in (0.1, 0.5, 0.9)]
+    # one cache sized for the longest context, filled once (cache contents do not change the
+    # work; random fill of ~19 GB would dominate the sample)
+    kv = zonos_ref.KVCache(cfg, 2 * B, max(ctxs) + 1)
+    for layer in kv.kv:
+        layer.fill_(0.01)
+    t_setup = time.time() - t_begin
+    for ctx in ctxs:
         ids = torch.randint(0, 1024, (2 * B, 9, 1))
         for _ in range(args.cpu_sample_steps):
+            kv.seqlen_offset = ctx
+            kv.lengths[:] = ctx
             t = time.time()
             with torch.no_grad():
                 zonos_ref.compute_logits(W, cfg, zonos_ref.embed_codes(W, cfg, ids), kv, freqs, 2.0)
             times.append(time.time() - t)
-            kv.seqlen_offset = ctx
-            kv.lengths[:] = ctx
     step_s = sum(times) / len(times)
     dW = dac_ref.make_dac_weights(dac_ref.DAC_44KHZ, seed=0)
     T = 43
@@ -128,7 +131,7 @@ def cpu_baseline(args):
                 sample=f"oracle decode step B={B} at ctx {ctx0 + int(0.1 * N)}/{ctx0 + int(0.5 * N)}/"
                        f"{ctx0 + int(0.9 * N)} x{args.cpu_sample_steps} (mean {step_s:.3f} s/step) + DAC 43 frames "
                        f"({dac_s_per_frame * 1e3:.1f} ms/frame); scaled to {N} steps + {B * args.new_tokens} frames; "
-                       f"{time.time() - t_begin:.1f} s of CPU work",
+                       f"{time.time() - t_begin - t_setup:.1f} s of timed CPU work (+{t_setup:.1f} s setup)",
                 step_s=round(step_s, 4), dac_ms_per_frame=round(dac_s_per_frame * 1e3, 2))
 
 
@@ -217,6 +220,7 @@ def main():
             "rtf": round(audio_s / elapsed, 2),
             "breakdown": {"generate_s_per_step": round(stats["gen_s"] / args.steps, 3),
                           "dac_s_per_step": round(stats["dac_s"] / args.steps, 3),
+                          "dac_precision": dac.precision if dac is not None else None,
                           "generate_codes_s": round(frames / world * 9 / max(stats["gen_s"], 1e-9) * world, 1),
                           "decode_ms_per_token_step": round(stats["gen_s"] / args.steps / (args.new_tokens + 8) * 1e3,
                                                             3)},

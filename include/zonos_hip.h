@@ -191,7 +191,8 @@ int zk_dac_prep_convt(const float* w, int Cin, int Cout, int s, float* w_out, vo
  * operands (the reference's own GPU numerics: autocast fp16, autoencoder.py:46).
  * Weights prepacked by zk_dac_prep_w16: mode 0 conv [Cout][Cin][ks] -> [ks][Cout][Cin];
  * mode 1 ConvTranspose1d [Cin][Cout][2s] -> [s][2][Cout][Cin] (phase r at offset 2*r*Cout*Cin,
- * run with ks=2, dil=1, pad=1, out_stride=s, out_off=r-ceil(s/2)). Cin % 32 == 0. */
+ * run with ks=2, dil=1, pad=1, out_stride=s, out_off=r-ceil(s/2)). Cin % 32 == 0. w_lo may be
+ * NULL (plain fp16 packing). */
 int zk_dac_prep_w16(const float* w, int Cout, int Cin, int ks, int s, int mode, uint16_t* w_hi,
                     uint16_t* w_lo, void* stream);
 int zk_dac_conv16(const float* in, int B, int Cin, int Tin, const float* alpha, const uint16_t* w_hi,
@@ -201,6 +202,31 @@ int zk_dac_conv16(const float* in, int B, int Cin, int Tin, const float* alpha, 
 /* Final Snake -> Conv1d(C -> 1, k7, pad 3) -> tanh (modeling_dac.py:437-439); out [B][T]. */
 int zk_dac_tail(const float* in, int B, int C, int T, const float* alpha, const float* w,
                 const float* bias, float* out, const int32_t* lens, int scale, void* stream);
+
+/* ---- channels-last fp16 pipeline (default "fp16" precision; dac_cl.hip). Activations are
+ * s = fp16(Snake(x)) [B][T][C] with C padded to a multiple of 32 (zero channels), the
+ * residual stream x fp32 [B][T][C]. Each conv applies the NEXT Snake in its epilogue. */
+/* z[b][t][ch] = fp16(sum_k E_k[codes[b][k][t]][ch]) (k ascending), channels [hidden, cpad) = 0. */
+int zk_dac_rvq_decode_cl(const int64_t* codes, int B, int ncb, int T, long code_bstride,
+                         const float* tables, int ncode, int hidden, int cpad, uint16_t* z,
+                         const int32_t* lens, void* stream);
+/* For q < Qn, phase r < nphase, t = q*out_stride + out_off0 + r in [0, Tout):
+ *   v = bias[co] + sum_{ci,k} W_r[k][co][ci] * in[b][q + k*dil - pad][ci]  (+ resid[b][t][co])
+ *   x_out[b][t][co] = v (if x_out);  s_out[b][t][co] = fp16(Snake_{alpha_next}(v))
+ *   (s_f32 = 1: s_out is fp32 and the Snake uses the exact sinf -- the input of zk_dac_tail_cl)
+ * W_r = w + r*w_phase_stride (zk_dac_prep_w16 hi layout). Inputs outside [0, lens[b]*in_scale)
+ * read 0; outputs at t >= lens[b]*out_scale are written 0. Cin, Cout % 32 == 0; ks <= 7,
+ * (ks-1)*dil <= 64. Conv1d: nphase=1, out_stride=1, out_off0=0. ConvTranspose1d(stride s):
+ * ks=2, dil=1, pad=1, Qn=Tin+1, nphase=s, out_stride=s, out_off0=-ceil(s/2). */
+int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* w, long w_phase_stride,
+                   const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
+                   int out_stride, int out_off0, int Tout, const float* resid, float* x_out,
+                   const float* alpha_next, void* s_out, int s_f32, const int32_t* lens, int in_scale,
+                   int out_scale, void* stream);
+/* out[b][t] = tanh(bias + sum_{c,k} w[c*7+k] * s[b][t+k-3][c]), 0 at t >= lens[b]*scale
+ * (s = fp32 output of the final Snake, zk_dac_conv_cl with s_f32 = 1; modeling_dac.py:437-439). */
+int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias,
+                   float* out, const int32_t* lens, int scale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -67,6 +67,9 @@ _SIGS = {
     "zk_dac_prep_w16": [P, I, I, I, I, I, P, P, P],
     "zk_dac_conv16": [P, I, I, I, P, P, P, P, I, I, I, I, I, I, I, P, I, P, I, P, I, I, I, P],
     "zk_dac_tail": [P, I, I, I, P, P, P, P, P, I, P],
+    "zk_dac_rvq_decode_cl": [P, I, I, I, L, P, I, I, I, P, P, P],
+    "zk_dac_conv_cl": [P, I, I, I, P, L, P, I, I, I, I, I, I, I, I, I, P, P, P, P, I, P, I, I, P],
+    "zk_dac_tail_cl": [P, I, I, I, P, P, P, P, I, P],
 }
 
 _lib = None
@@ -101,6 +104,8 @@ def exported_symbols() -> list[str]:
 
 def call(name: str, *args):
     lib = load()
+    if len(args) != len(_SIGS[name]):
+        raise TypeError(f"{name}: {len(args)} arguments given, the C ABI takes {len(_SIGS[name])}")
     rc = getattr(lib, name)(*args)
     if rc != 0:
         raise ZonosHipError(f"{name} failed ({rc}): {lib.zk_last_error().decode()}")

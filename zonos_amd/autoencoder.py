@@ -63,11 +63,13 @@ def _fold_weight_norm(sd: dict) -> dict:
 class HipDacDecoder:
     """Decoder weights on the device + the launch sequence of the DAC decoder.
 
-    precision: "fp16x3" (default; split-precision fp16 MFMA, ~fp32 accuracy), "fp16" (plain
-    fp16 operands = the reference's GPU autocast numerics, 3x less MFMA work) or "fp32"
-    (exact-fp32 MFMA kernel, slowest)."""
+    precision: "fp16" (default; the reference's own GPU numerics -- autocast fp16 around
+    DacModel.decode, autoencoder.py:46 -- on the channels-last pipeline of dac_cl.hip: fp16
+    conv operands, fp32 accumulation and fp32 residual stream), "fp16x3" (split-precision
+    fp16 MFMA, ~fp32 accuracy) or "fp32" (exact-fp32 MFMA kernel); the last two match the
+    reference's CPU fp32 decode to ~1e-6 RMS and run channels-first."""
 
-    def __init__(self, spec: DacSpec, state_dict: dict, device="cuda", precision: str = "fp16x3"):
+    def __init__(self, spec: DacSpec, state_dict: dict, device="cuda", precision: str = "fp16"):
         _lib.load()
         assert precision in ("fp16x3", "fp16", "fp32"), precision
         self.precision = precision
@@ -90,9 +92,11 @@ class HipDacDecoder:
              s.n_codebooks, s.codebook_size, s.codebook_dim, s.hidden_size, ptr(self.tables), stream)
         self.conv1_w, self.conv1_b = t("decoder.conv1.weight"), t("decoder.conv1.bias")
         self.blocks = []
+        self._convt_raw = []
         for i, st in enumerate(s.upsampling_ratios):
             p = f"decoder.block.{i}."
             wt = t(p + "conv_t1.weight")                      # [Cin][Cout][2s]
+            self._convt_raw.append(wt)
             cin, cout = wt.shape[0], wt.shape[1]
             wprep = torch.empty(st, cout, cin, 2, device=dev)
             call("zk_dac_prep_convt", ptr(wt), cin, cout, st, ptr(wprep), stream)
@@ -106,7 +110,9 @@ class HipDacDecoder:
             self.blocks.append(blk)
         self.final_alpha = t("decoder.snake1.alpha").reshape(-1)
         self.conv2_w, self.conv2_b = t("decoder.conv2.weight"), t("decoder.conv2.bias")
-        if precision != "fp32":
+        if precision == "fp16":
+            self._prep_cl(stream)
+        elif precision != "fp32":
             self.w16 = {}
             self._prep16("conv1", self.conv1_w, 0, stream)
             for i, blk in enumerate(self.blocks):
@@ -115,6 +121,103 @@ class HipDacDecoder:
                     self._prep16(f"b{i}.r{j}.1", ru["w1"], 0, stream)
                     self._prep16(f"b{i}.r{j}.2", ru["w2"], 0, stream)
         torch.cuda.synchronize(dev)
+
+    # ---------------------------------------------------------------- channels-last fp16 path
+    @staticmethod
+    def _pad32(c):
+        return (c + 31) // 32 * 32
+
+    def _prep_cl(self, stream):
+        """Weights for dac_cl.hip: channels zero-padded to multiples of 32, fp16 [tap][Cout][Cin]
+        (ConvTranspose1d: [phase][2][Cout][Cin]); biases padded with 0, Snake alphas with 1."""
+        dev, s, P = self.device, self.spec, self._pad32
+
+        def wconv(w):                       # [Cout][Cin][ks] -> fp16 [ks][Cout_p][Cin_p]
+            co, ci, ks = w.shape
+            wp = torch.zeros(P(co), P(ci), ks, device=dev)
+            wp[:co, :ci] = w
+            out = torch.empty(ks * P(co) * P(ci), dtype=torch.int16, device=dev)
+            call("zk_dac_prep_w16", ptr(wp), P(co), P(ci), ks, 1, 0, ptr(out), None, stream)
+            return out
+
+        def wconvt(w, st):                  # [Cin][Cout][2s] -> fp16 [s][2][Cout_p][Cin_p]
+            ci, co, _ = w.shape
+            wp = torch.zeros(P(ci), P(co), 2 * st, device=dev)
+            wp[:ci, :co] = w
+            out = torch.empty(st * 2 * P(co) * P(ci), dtype=torch.int16, device=dev)
+            call("zk_dac_prep_w16", ptr(wp), P(co), P(ci), 2, st, 1, ptr(out), None, stream)
+            return out
+
+        def vec(v, fill):
+            out = torch.full((P(v.numel()),), fill, device=dev)
+            out[:v.numel()] = v.reshape(-1)
+            return out
+
+        cl = {"cin0": P(s.hidden_size), "c0": P(self.conv1_w.shape[0]), "conv1_w": wconv(self.conv1_w),
+              "conv1_b": vec(self.conv1_b, 0.0), "blocks": []}
+        for blk in self.blocks:
+            st = blk["stride"]
+            b = {"stride": st, "cin": P(blk["cin"]), "cout": P(blk["cout"]), "alpha": vec(blk["alpha"], 1.0),
+                 "wt": wconvt(self._convt_raw[len(cl["blocks"])], st), "bt": vec(blk["bt"], 0.0), "res": []}
+            for ru in blk["res"]:
+                b["res"].append({"dil": ru["dil"], "a1": vec(ru["a1"], 1.0), "w1": wconv(ru["w1"]),
+                                 "b1": vec(ru["b1"], 0.0), "a2": vec(ru["a2"], 1.0), "w2": wconv(ru["w2"]),
+                                 "b2": vec(ru["b2"], 0.0)})
+            cl["blocks"].append(b)
+        cl["final_alpha"] = vec(self.final_alpha, 1.0)
+        cw = torch.zeros(P(self.conv2_w.shape[1]), 7, device=dev)
+        cw[:self.conv2_w.shape[1]] = self.conv2_w[0]
+        cl["conv2_w"], cl["conv2_b"] = cw.contiguous(), self.conv2_b.contiguous()
+        self.cl = cl
+
+    def _decode_cl(self, codes, lens, stream):
+        s, cl, dev = self.spec, self.cl, self.device
+        B, K, T = codes.shape
+        f16 = torch.int16
+        z = torch.empty(B, T, cl["cin0"], dtype=f16, device=dev)
+        call("zk_dac_rvq_decode_cl", ptr(codes), B, K, T, K * T, ptr(self.tables), s.codebook_size, s.hidden_size,
+             cl["cin0"], ptr(z), ptr(lens), stream)
+        blocks = cl["blocks"]
+        a_next = blocks[0]["alpha"] if blocks else cl["final_alpha"]
+        act = torch.empty(B, T, cl["c0"], dtype=f16, device=dev)
+        call("zk_dac_conv_cl", ptr(z), B, cl["cin0"], T, ptr(cl["conv1_w"]), 0, ptr(cl["conv1_b"]), cl["c0"], 7, 1, 3,
+             T, 1, 1, 0, T, None, None, ptr(a_next), ptr(act), 0, ptr(lens), 1, 1, stream)
+        del z
+        L, scale = T, 1
+        for bi, blk in enumerate(blocks):
+            st, cin, cout = blk["stride"], blk["cin"], blk["cout"]
+            Lo = L * st
+            x = torch.empty(B, Lo, cout, device=dev)
+            s_new = torch.empty(B, Lo, cout, dtype=f16, device=dev)
+            a1 = blk["res"][0]["a1"]
+            call("zk_dac_conv_cl", ptr(act), B, cin, L, ptr(blk["wt"]), 2 * cout * cin, ptr(blk["bt"]), cout, 2, 1, 1,
+                 L + 1, st, st, -((st + 1) // 2), Lo, None, ptr(x), ptr(a1), ptr(s_new), 0, ptr(lens), scale,
+                 scale * st, stream)
+            act = s_new
+            scale *= st
+            L = Lo
+            tmp = torch.empty_like(act)
+            nres = len(blk["res"])
+            for j, ru in enumerate(blk["res"]):
+                d = ru["dil"]
+                if j + 1 < nres:
+                    a_next = blk["res"][j + 1]["a1"]
+                elif bi + 1 < len(blocks):
+                    a_next = blocks[bi + 1]["alpha"]
+                else:
+                    a_next = cl["final_alpha"]
+                call("zk_dac_conv_cl", ptr(act), B, cout, L, ptr(ru["w1"]), 0, ptr(ru["b1"]), cout, 7, d, 3 * d, L,
+                     1, 1, 0, L, None, None, ptr(ru["a2"]), ptr(tmp), 0, ptr(lens), scale, scale, stream)
+                last = j + 1 == nres and bi + 1 == len(blocks)
+                if last:       # the tail's input: fp32 Snake output (keeps the waveform at fp32-level error)
+                    act = torch.empty(B, L, cout, device=dev)
+                call("zk_dac_conv_cl", ptr(tmp), B, cout, L, ptr(ru["w2"]), 0, ptr(ru["b2"]), cout, 1, 1, 0, L,
+                     1, 1, 0, L, ptr(x), ptr(x), ptr(a_next), ptr(act), int(last), ptr(lens), scale, scale, stream)
+            del tmp, x
+        out = torch.empty(B, 1, L, device=dev)
+        call("zk_dac_tail_cl", ptr(act), B, act.shape[2], L, ptr(cl["conv2_w"]), ptr(cl["conv2_b"]), ptr(out),
+             ptr(lens), scale, stream)
+        return out
 
     def _prep16(self, key, w, mode, stream, s=1):
         if mode == 0:
@@ -154,6 +257,8 @@ class HipDacDecoder:
         stream = _lib.stream_ptr(dev)
         if lens is not None:
             lens = lens.to(device=dev, dtype=torch.int32).contiguous()
+        if self.precision == "fp16":
+            return self._decode_cl(codes, lens, stream)
         z = torch.empty(B, s.hidden_size, T, device=dev)
         call("zk_dac_rvq_decode", ptr(codes), B, K, T, K * T, ptr(self.tables), s.codebook_size, s.hidden_size,
              ptr(z), T, ptr(lens), stream)
@@ -193,9 +298,9 @@ class HipDacDecoder:
                  ptr(out), ptr(lens), scale, stream)
         return out
 
-    def decode_list(self, codes_list, max_batch_elems: float = 6e9) -> list:
+    def decode_list(self, codes_list, max_batch_bytes: float = 64e9) -> list:
         """Per-utterance waveforms for a list of [9, T_i] / [1, 9, T_i] code tensors, decoded as
-        zero-padded batches (chunks bounded by activation memory)."""
+        zero-padded batches (chunks bounded by activation memory, default 64 GB of HBM)."""
         items = []
         for c in codes_list:
             c = c.unsqueeze(0) if c.dim() == 2 else c
@@ -209,7 +314,10 @@ class HipDacDecoder:
         i = 0
         while i < len(order):
             Tmax = items[order[i]].shape[1]
-            per = max(1, int(max_batch_elems // (3 * width * hop * Tmax)))
+            # live activations at the widest-time stage: channels-last fp32 x + 2 fp16 (+ the
+            # previous stage's fp16 input) ~ 10 B per (position, channel); channels-first fp32 ~ 12 B
+            per_bytes = (10 if self.precision == "fp16" else 12) * self._pad32(width) * hop * Tmax
+            per = max(1, int(max_batch_bytes // per_bytes))
             grp = order[i:i + per]
             codes = torch.zeros(len(grp), self.spec.n_codebooks, Tmax, dtype=torch.int64, device=self.device)
             lens = torch.tensor([items[g].shape[1] for g in grp], dtype=torch.int32)

@@ -1,0 +1,381 @@
+// DAC decoder, channels-last fp16 pipeline (the default "fp16" precision: the numerics of the
+// reference's own GPU path, torch.autocast fp16 around DacModel.decode, autoencoder.py:46 --
+// fp16 conv operands, fp32 accumulation; here the residual stream additionally stays fp32).
+//
+// Layout: every conv reads s = fp16(Snake(x)) as [B][T][C] (channels-last, C padded to a
+// multiple of 32 with zero channels) and its epilogue applies the NEXT Snake, so the conv
+// main loop is pure data movement + MFMA:
+//   conv7(res unit)   : s' = Snake_a2(conv + b)                      (fp16 out only)
+//   conv1(res unit)   : x  = x + conv + b ; s = Snake_next(x)         (fp32 x + fp16 s)
+//   ConvTranspose1d   : x  = conv + b     ; s = Snake_res1(x)         (s polyphase 2-tap convs)
+//   first conv        : s = Snake_block0(conv + b)
+// (modeling_dac.py:95-100 Snake, :222-233 residual unit, :266-278 decoder block, :420-439).
+//
+// Implicit GEMM on v_mfma_f32_16x16x32_f16: M = output channels, N = positions, K = (tap,
+// input channel). Workgroup tile CO_T = 32*FM channels x QT = 128 positions, 4 waves as 2x2,
+// each wave (16*FM) x 64. K is walked as steps (channel chunk c of CI, tap t): per chunk the
+// input window (QT + (ks-1)*dil positions x CI channels) is staged once and reused by all
+// taps (tap t reads rows shifted by t*dil); the (tap, chunk) weight slice is staged per step.
+// Both images land in LDS by LDS-DMA (global_load_lds_dwordx4, lane-linear destination, XOR
+// swizzle of the 16-B channel groups applied on the source address); out-of-range positions
+// read a zero page, which is the conv's zero padding AND the per-row length masking of a
+// ragged batch. A dedicated loader wave keeps several weight slices and windows in flight
+// (LDS rings, counted vmcnt, one raw s_barrier per step); the 4 compute waves never load.
+#include "common.h"
+#include "../../include/zonos_hip.h"
+#include <algorithm>
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int QT = 128;          // positions per workgroup
+constexpr int MAXSPAN = 64;      // max (ks-1)*dil
+
+__device__ __attribute__((aligned(256))) uint4 g_zero_page[16];   // 256 zero bytes (LDS-DMA source for padding)
+
+template <int CI>
+struct Img {                      // [rows][CI fp16] image, 16-B groups XOR-swizzled per 256-B bank row
+    static constexpr int G = CI / 8;
+    static constexpr int RB = CI * 2;
+    static constexpr int RPB = 256 / RB;
+    static constexpr int RPR = 4096 / RB;        // rows per load round (256 lanes x 16 B)
+    ZK_DEV static int swz(int row) { return (int)(((unsigned)row / RPB) % G); }
+    ZK_DEV static int off(int row, int g) { return row * RB + ((g ^ swz(row)) << 4); }
+};
+
+ZK_DEV f16x8 as_h8(uint4 v) { return __builtin_bit_cast(f16x8, v); }
+
+ZK_DEV float snake(float x, float a) {     // x + 1/(a + 1e-9) * sin(a x)^2   (modeling_dac.py:95-100)
+    const float s = sinf(__fmul_rn(a, x));
+    return __fadd_rn(x, __fmul_rn(__fdiv_rn(1.0f, __fadd_rn(a, 1e-9f)), __fmul_rn(s, s)));
+}
+
+// fp16-output Snake: hardware sine (abs. error ~1e-6 at these arguments, far below the fp16
+// rounding of the result) and a per-channel reciprocal.
+ZK_DEV float snake_fast(float x, float a, float ra) {
+    const float s = __sinf(a * x);
+    return fmaf(ra, s * s, x);
+}
+
+ZK_DEV uint2 pack_h4(float a, float b, float c, float d) {
+    _Float16 h[4] = {(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)d};
+    return *reinterpret_cast<const uint2*>(h);
+}
+
+// s_waitcnt vmcnt(n) for a runtime n (clamped to the 6-bit field): a jump table of immediates.
+ZK_DEV void wait_vm(int n) {
+#define ZK_W1(N_) case N_: asm volatile("s_waitcnt vmcnt(" #N_ ")" ::: "memory"); break;
+#define ZK_W8(B_) ZK_W1(B_ + 0) ZK_W1(B_ + 1) ZK_W1(B_ + 2) ZK_W1(B_ + 3) ZK_W1(B_ + 4) ZK_W1(B_ + 5) ZK_W1(B_ + 6) ZK_W1(B_ + 7)
+    switch (n < 0 ? 0 : (n > 63 ? 63 : n)) {
+        ZK_W8(0) ZK_W8(8) ZK_W8(16) ZK_W8(24) ZK_W8(32) ZK_W8(40) ZK_W8(48) ZK_W8(56)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef ZK_W8
+#undef ZK_W1
+}
+
+constexpr int CL_DA = 3;                 // weight slices in flight ahead of the step being computed
+constexpr int CL_NW = CL_DA + 2;         // weight ring slots
+constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
+
+// Loader-wave implicit GEMM. Wave 4 only moves bytes (LDS-DMA) and counts its own vmcnt;
+// waves 0-3 only read LDS + MFMA, so the vmcnt(0) that hipcc places before their ds_reads
+// (it cannot tell the DMA's LDS range) costs nothing -- they have no loads in flight.
+// Step i = (chunk c, tap t); the loader runs CL_DA steps ahead for weights and DX steps
+// ahead for windows (DX >= CL_DA, window ring of NX slots), one raw s_barrier per step.
+template <int FM>
+__global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
+    const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
+    const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
+    int out_off0, int Tout, const float* resid, float* xout, const float* __restrict__ alpha,
+    void* __restrict__ sout, int s_f32, const int32_t* __restrict__ lens, int in_scale, int out_scale, int nq,
+    int nx_slots, int dx) {
+    constexpr int CI = 32;
+    using I = Img<CI>;
+    constexpr int CO_T = 32 * FM;
+    constexpr int WS = CO_T * I::RB;             // weight slot bytes
+    constexpr int NWP = CO_T / 16;               // weight pieces (1 KiB = 16 rows) per step
+    extern __shared__ __attribute__((aligned(16))) char smem[];   // [W ring][X ring], one array
+
+    // XCD-aware decode of the 1-D grid: the workgroups an XCD receives (ids = xcd mod 8) walk
+    // co-tiles fastest, so one window is re-read from that XCD's L2 rather than from HBM.
+    const int nco = (Cout / CO_T) * nphase;
+    const int nwg = gridDim.x, id = blockIdx.x;
+    const int xcd = id & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int L = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (id >> 3);
+    const int cot = L % nco, qtile = (L / nco) % nq, b = L / (nco * nq);
+    const int phase = cot % nphase, co0 = (cot / nphase) * CO_T;
+    const int q0 = qtile * QT;
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int win = QT + (ks - 1) * dil;
+    const int nxp = (win + 15) >> 4;             // window pieces (16 rows each)
+    const int XS = nxp * 1024;
+    char* const wring = smem;
+    char* const xring = smem + CL_NW * WS;
+    const int nchunk = Cin / CI, nstep = nchunk * ks;
+
+    if (wv == 4) {
+        // ---------------- loader wave
+        const int len_in = lens ? min(lens[b] * in_scale, Tin) : Tin;
+        const uint16_t* wp = w + (size_t)phase * wphase;
+        const size_t wtap = (size_t)Cout * Cin;
+        const uint16_t* inb = in + (size_t)b * Tin * Cin;
+        const int u0 = q0 - pad;
+        const int prow = lane >> 2, pslot = lane & 3;   // a 1 KiB piece = 16 rows x 4 slots
+        int hist[CL_DA + 1] = {};                       // loads issued by iterations j-CL_DA .. j
+        for (int j = -dx; j < nstep; ++j) {
+            int nl = 0;
+            // window first: a window issued in the same iteration as W(j+CL_DA) is then older
+            // than it, so waiting for W(j) below also covers every window step j can need
+            const int sx = j + dx;
+            if (sx >= 0 && sx < nstep && sx % ks == 0) {
+                const int c = sx / ks;
+                char* dst = xring + (c % nx_slots) * XS;
+                for (int p = 0; p < nxp; ++p) {
+                    const int row = p * 16 + prow;
+                    const int u = u0 + row;
+                    const int g = pslot ^ I::swz(row);
+                    const void* src = (row < win && u >= 0 && u < len_in)
+                                          ? (const void*)(inb + (size_t)u * Cin + c * CI + g * 8)
+                                          : (const void*)g_zero_page;
+                    __builtin_amdgcn_global_load_lds(src, (void*)(dst + p * 1024), 16, 0, 0);
+                }
+                nl += nxp;
+            }
+            const int sw = j + CL_DA;
+            if (sw >= 0 && sw < nstep) {
+                const int c = sw / ks, t = sw - c * ks;
+                char* dst = wring + (sw % CL_NW) * WS;
+                const uint16_t* src0 = wp + t * wtap + (size_t)co0 * Cin + c * CI;
+#pragma unroll
+                for (int p = 0; p < NWP; ++p) {
+                    const int row = p * 16 + prow;
+                    const int g = pslot ^ I::swz(row);
+                    __builtin_amdgcn_global_load_lds((const void*)(src0 + (size_t)row * Cin + g * 8),
+                                                     (void*)(dst + p * 1024), 16, 0, 0);
+                }
+                nl += NWP;
+            }
+#pragma unroll
+            for (int k = 0; k < CL_DA; ++k) hist[k] = hist[k + 1];
+            hist[CL_DA] = nl;
+            if (j >= 0) {
+                // step j needs W(j), issued by iteration j - CL_DA; everything issued later may stay in flight
+                int pend = 0;
+#pragma unroll
+                for (int k = 1; k <= CL_DA; ++k) pend += hist[k];
+                wait_vm(pend);
+                __builtin_amdgcn_s_barrier();           // publish step j
+            }
+        }
+        return;
+    }
+
+    // ---------------- compute waves 0-3: 2 (co) x 2 (positions)
+    const int ln = lane & 15, lg = lane >> 4, wm = wv >> 1, wn = wv & 1;
+    f32x4 acc[FM][4];
+#pragma unroll
+    for (int m = 0; m < FM; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int s = 0; s < nstep; ++s) {
+        const int c = s / ks, t = s - c * ks;
+        __builtin_amdgcn_s_barrier();            // step s is in LDS
+        asm volatile("" ::: "memory");
+        const char* xb = xring + (c % nx_slots) * XS;
+        const char* wb = wring + (s % CL_NW) * WS;
+        uint4 a[FM], bq[4];
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+            a[m] = *reinterpret_cast<const uint4*>(wb + I::off(wm * 16 * FM + m * 16 + ln, lg));
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+            bq[n] = *reinterpret_cast<const uint4*>(xb + I::off(wn * 64 + n * 16 + ln + t * dil, lg));
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a[m]), as_h8(bq[n]), acc[m][n], 0, 0, 0);
+    }
+
+    // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 64wn + 16n + ln]
+    const int len_out = lens ? lens[b] * out_scale : Tout;
+    const int out_off = out_off0 + phase;
+#pragma unroll
+    for (int m = 0; m < FM; ++m) {
+        const int co = co0 + wm * 16 * FM + m * 16 + lg * 4;
+        const float4 bb = *reinterpret_cast<const float4*>(bias + co);
+        const float4 aa = *reinterpret_cast<const float4*>(alpha + co);
+        const float r0 = __fdiv_rn(1.0f, __fadd_rn(aa.x, 1e-9f)), r1 = __fdiv_rn(1.0f, __fadd_rn(aa.y, 1e-9f));
+        const float r2 = __fdiv_rn(1.0f, __fadd_rn(aa.z, 1e-9f)), r3 = __fdiv_rn(1.0f, __fadd_rn(aa.w, 1e-9f));
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int q = q0 + wn * 64 + n * 16 + ln;
+            const int tt = q * out_stride + out_off;
+            if (q >= Qn || tt < 0 || tt >= Tout) continue;
+            const size_t o = ((size_t)b * Tout + tt) * Cout + co;
+            float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+            if (tt < len_out) {
+                v0 = __fadd_rn(acc[m][n][0], bb.x);
+                v1 = __fadd_rn(acc[m][n][1], bb.y);
+                v2 = __fadd_rn(acc[m][n][2], bb.z);
+                v3 = __fadd_rn(acc[m][n][3], bb.w);
+                if (resid) {
+                    const float4 r = *reinterpret_cast<const float4*>(resid + o);
+                    v0 = __fadd_rn(r.x, v0);
+                    v1 = __fadd_rn(r.y, v1);
+                    v2 = __fadd_rn(r.z, v2);
+                    v3 = __fadd_rn(r.w, v3);
+                }
+            }
+            if (xout) *reinterpret_cast<float4*>(xout + o) = make_float4(v0, v1, v2, v3);
+            if (s_f32)      // fp32 Snake output for the fp32 tail (exact sinf, reference formula)
+                reinterpret_cast<float4*>(sout)[o >> 2] =
+                    make_float4(snake(v0, aa.x), snake(v1, aa.y), snake(v2, aa.z), snake(v3, aa.w));
+            else
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(sout) + o) =
+                    pack_h4(snake_fast(v0, aa.x, r0), snake_fast(v1, aa.y, r1), snake_fast(v2, aa.z, r2),
+                            snake_fast(v3, aa.w, r3));
+        }
+    }
+}
+
+// z[b][t][ch] = fp16(sum_k E_k[code_k][ch]) channels-last, zero beyond the row's length
+// (quantizer.from_codes, modeling_dac.py:520-538; summation order k = 0..ncb-1 as there).
+__global__ __launch_bounds__(256) void k_rvq_cl(const int64_t* __restrict__ codes, int ncb, int T, long bstr,
+                                                const float* __restrict__ tables, int ncode, int hidden, int cpad,
+                                                uint16_t* __restrict__ z, const int32_t* __restrict__ lens) {
+    const int t = blockIdx.x, b = blockIdx.y;
+    const int len = lens ? lens[b] : T;
+    for (int ch = threadIdx.x * 4; ch < cpad; ch += 1024) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        if (t < len && ch < hidden) {
+            for (int k = 0; k < ncb; ++k) {
+                int64_t cd = codes[b * bstr + (size_t)k * T + t];
+                cd = cd < 0 ? 0 : (cd >= ncode ? ncode - 1 : cd);
+                const float4 e = *reinterpret_cast<const float4*>(tables + ((size_t)k * ncode + cd) * hidden + ch);
+                if (k == 0) {
+                    s[0] = e.x; s[1] = e.y; s[2] = e.z; s[3] = e.w;
+                } else {
+                    s[0] = __fadd_rn(s[0], e.x); s[1] = __fadd_rn(s[1], e.y);
+                    s[2] = __fadd_rn(s[2], e.z); s[3] = __fadd_rn(s[3], e.w);
+                }
+            }
+        }
+        *reinterpret_cast<uint2*>(z + ((size_t)b * T + t) * cpad + ch) = pack_h4(s[0], s[1], s[2], s[3]);
+    }
+}
+
+// out[b][t] = tanh(b + sum_{c,k} w[c][k] s[t+k-3][c]) from the channels-last fp32 Snake output
+// of the last residual unit (modeling_dac.py:437-439; one output channel, so VALU: an MFMA
+// tile would be 1/16 used). fp32 here keeps the waveform within the fp32 reference's 1e-4.
+constexpr int TAIL_T = 256;
+__global__ __launch_bounds__(256) void k_tail_cl(const float* __restrict__ s, int C, int T,
+                                                 const float* __restrict__ w, const float* __restrict__ bias,
+                                                 float* __restrict__ out, const int32_t* __restrict__ lens, int scale) {
+    extern __shared__ float wl[];            // [C][7]
+    for (int i = threadIdx.x; i < C * 7; i += 256) wl[i] = w[i];
+    __syncthreads();
+    const int b = blockIdx.y, t = blockIdx.x * TAIL_T + threadIdx.x;
+    if (t >= T) return;
+    const int len = lens ? min(lens[b] * scale, T) : T;
+    float acc = 0.f;
+    for (int k = 0; k < 7; ++k) {
+        const int u = t + k - 3;
+        if (u < 0 || u >= len) continue;
+        const float* row = s + ((size_t)b * T + u) * C;
+        for (int c = 0; c < C; c += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(row + c);
+            acc = fmaf(wl[(c + 0) * 7 + k], v.x, acc);
+            acc = fmaf(wl[(c + 1) * 7 + k], v.y, acc);
+            acc = fmaf(wl[(c + 2) * 7 + k], v.z, acc);
+            acc = fmaf(wl[(c + 3) * 7 + k], v.w, acc);
+        }
+    }
+    out[(size_t)b * T + t] = (t < len) ? tanhf(__fadd_rn(acc, bias[0])) : 0.f;
+}
+
+template <int FM>
+void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Cin, int Tin, const uint16_t* w,
+                 long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
+                 int out_stride, int out_off0, int Tout, const float* resid, float* xout, const float* alpha,
+                 void* sout, int s_f32, const int32_t* lens, int in_scale, int out_scale, int nq, int nx, int dx) {
+    if (lds > 65536)
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv_cl<FM>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+    hipLaunchKernelGGL((k_conv_cl<FM>), dim3(nwg), dim3(CL_THREADS), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
+                       dil, pad, Qn, nphase, out_stride, out_off0, Tout, resid, xout, alpha, sout, s_f32, lens,
+                       in_scale, out_scale, nq, nx, dx);
+}
+
+}  // namespace
+
+extern "C" int zk_dac_rvq_decode_cl(const int64_t* codes, int B, int ncb, int T, long code_bstride,
+                                    const float* tables, int ncode, int hidden, int cpad, uint16_t* z,
+                                    const int32_t* lens, void* stream) {
+    ZK_REQUIRE(hidden % 4 == 0 && cpad >= hidden && cpad % 32 == 0, "zk_dac_rvq_decode_cl: hidden=%d cpad=%d", hidden,
+               cpad);
+    if (B == 0 || T == 0) return 0;
+    hipLaunchKernelGGL(k_rvq_cl, dim3(T, B), dim3(256), 0, (hipStream_t)stream, codes, ncb, T, code_bstride, tables,
+                       ncode, hidden, cpad, z, lens);
+    ZK_CHECK_LAUNCH("zk_dac_rvq_decode_cl");
+    return 0;
+}
+
+extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* w, long w_phase_stride,
+                              const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
+                              int out_stride, int out_off0, int Tout, const float* resid, float* x_out,
+                              const float* alpha_next, void* s_out, int s_f32, const int32_t* lens, int in_scale,
+                              int out_scale, void* stream) {
+    ZK_REQUIRE(Cin > 0 && Cin % 32 == 0, "zk_dac_conv_cl: Cin=%d must be a multiple of 32", Cin);
+    ZK_REQUIRE(Cout > 0 && Cout % 32 == 0, "zk_dac_conv_cl: Cout=%d must be a multiple of 32", Cout);
+    ZK_REQUIRE(ks >= 1 && ks <= 7 && dil >= 1 && (ks - 1) * dil <= MAXSPAN, "zk_dac_conv_cl: ks=%d dil=%d", ks, dil);
+    ZK_REQUIRE(nphase >= 1 && alpha_next != nullptr && s_out != nullptr && bias != nullptr,
+               "zk_dac_conv_cl: bad arguments");
+    if (B == 0 || Qn <= 0) return 0;
+    const int nco = Cout / 32;
+    const int FM = nco % 4 == 0 ? 4 : (nco % 3 == 0 ? 3 : (nco % 2 == 0 ? 2 : 1));
+    const int win = QT + (ks - 1) * dil;
+    const size_t xs = (size_t)((win + 15) / 16) * 1024;
+    const size_t ws = (size_t)32 * FM * 64;
+    // window lead DX >= CL_DA steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
+    int dx = std::max(CL_DA, ks), nx = 1 + (dx + 1 + ks - 1) / ks;
+    while (dx > CL_DA && CL_NW * ws + nx * xs > 80 * 1024) {
+        --dx;
+        nx = 1 + (dx + 1 + ks - 1) / ks;
+    }
+    const size_t lds = CL_NW * ws + nx * xs;
+    ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_conv_cl: LDS %zu too large", lds);
+    const int nq = (Qn + QT - 1) / QT;
+    const long nwg = (long)B * nq * (Cout / (32 * FM)) * nphase;
+    ZK_REQUIRE(nwg < (1L << 31), "zk_dac_conv_cl: grid too large");
+    hipStream_t st = (hipStream_t)stream;
+#define ZK_CL(F_)                                                                                           \
+    launch_conv<F_>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad, Qn, nphase, \
+                    out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32, lens, in_scale, out_scale, nq, nx, dx)
+    switch (FM) {
+        case 4: ZK_CL(4); break;
+        case 3: ZK_CL(3); break;
+        case 2: ZK_CL(2); break;
+        default: ZK_CL(1); break;
+    }
+#undef ZK_CL
+    ZK_CHECK_LAUNCH("zk_dac_conv_cl");
+    return 0;
+}
+
+extern "C" int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias, float* out,
+                              const int32_t* lens, int scale, void* stream) {
+    ZK_REQUIRE(C > 0 && C % 4 == 0 && T >= 0, "zk_dac_tail_cl: bad shape C=%d", C);
+    if (B == 0 || T == 0) return 0;
+    const size_t lds = (size_t)C * 7 * sizeof(float);
+    ZK_REQUIRE(lds <= 64 * 1024, "zk_dac_tail_cl: C=%d too large", C);
+    hipLaunchKernelGGL(k_tail_cl, dim3((T + TAIL_T - 1) / TAIL_T, B), dim3(256), lds, (hipStream_t)stream, s, C, T, w,
+                       bias, out, lens, scale);
+    ZK_CHECK_LAUNCH("zk_dac_tail_cl");
+    return 0;
+}

@@ -187,7 +187,7 @@ __global__ void k_prep_w16(const float* w, int Cout, int Cin, int ks, int s, int
         const _Float16 h = (_Float16)v;
         const _Float16 l = (_Float16)(v - (float)h);
         hi[i] = __builtin_bit_cast(uint16_t, h);
-        lo[i] = __builtin_bit_cast(uint16_t, l);
+        if (lo) lo[i] = __builtin_bit_cast(uint16_t, l);
     }
 }
 
