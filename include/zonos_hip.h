@@ -116,6 +116,13 @@ int zk_attn_decode(const void* q, const void* k_cache, const void* vt_cache, int
                    void* out, const int32_t* skip, void* stream);
 int zk_attn_prefill(const void* q, const void* k_cache, const void* v_rows, int R, int S, int H,
                     int Hkv, int hd, int Smax, void* out, void* stream);
+/* Decode with the in_proj epilogue fused in (= zk_qkv_rope at pos = ctx-1, S = 1, followed by
+ * zk_attn_decode): reduces the in_proj slabs (gemm_nsplit x [R][(H+2Hkv)*hd] fp32), applies
+ * RoPE, writes the new K / V^T cache entries and attends over keys [0, ctx). q is not stored. */
+int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
+                       void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
+                       const int32_t* ctx_dev, float* work, int nsplit, void* out,
+                       const int32_t* skip, void* stream);
 
 /* ------------------------------------------------------------------ graphs and timing
  * The decode step is captured once into a hipGraph and replayed (the reference runs the

@@ -105,6 +105,17 @@ def test_generate_graph_equals_eager():
     assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
+def test_fused_qkv_attention_equals_separate_kernels():
+    """zk_attn_decode_qkv (in_proj epilogue inside the attention launch) computes the same
+    numbers as zk_qkv_rope + zk_attn_decode: identical codes, bit for bit."""
+    c = load_gen_case("sampled_cli")
+    eng = _engine(c["W"])
+    a = eng.generate(c["cond"].cuda(), c["prefix"].cuda(), c["max_new"], 2.0, c["B"], c["sp"], seed=9)
+    eng.fuse_qkv = False
+    b = eng.generate(c["cond"].cuda(), c["prefix"].cuda(), c["max_new"], 2.0, c["B"], c["sp"], seed=9)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+
+
 def test_teacher_forced_logits():
     """Prefill + first decode steps: fp32 CFG logits vs the reference (golden) within tolerance."""
     c = load_gen_case("greedy")

@@ -37,9 +37,10 @@ def gemm():
                              ("fc2", 2048, 8192, 0), ("heads", 9234, 2048, 0)):
         # distinct weight buffers per rep set so L2/MALL does not serve them: rotate 8 copies (>256 MB total)
         ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
-        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        Npad = (N + 63) // 64 * 64        # packed layout reads whole 64-row tiles
+        Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
         A = torch.randn(M, K, device=dev).to(torch.bfloat16)
-        ns = 1 if mode == 1 else _split_for(N, K, M)
+        ns = 1 if mode == 1 else _split_for(N, K, M, int(os.environ.get("ZK_SPLIT_TARGET", "256")))
         part = torch.empty(ns * M * N, device=dev)
         out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
         it = [0]

@@ -12,7 +12,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libzonos_hip.so")
+LIB_PATH = os.environ.get("ZK_LIB_PATH") or os.path.join(_HERE, "lib", "libzonos_hip.so")
 
 P = C.c_void_p
 I = C.c_int
@@ -49,6 +49,7 @@ _SIGS = {
     "zk_permute_fc1": [P, I, I, P, P],
     "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, P, P],
     "zk_attn_decode": [P, P, P, I, I, I, I, I, I, P, P, I, P, P, P],
+    "zk_attn_decode_qkv": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, P, P, P],
     "zk_attn_prefill": [P, P, P, I, I, I, I, I, I, P, P],
     "zk_sample_heads": [P, I, C.POINTER(GenState), C.POINTER(SamplingParams), I, I, P, P],
     "zk_eos_step": [C.POINTER(GenState), I, I, P],

@@ -29,9 +29,9 @@ def _deps_mtime() -> float:
     return max(os.path.getmtime(f) for f in files)
 
 
-def _compile(src: str) -> str:
-    obj = os.path.join(LIBDIR, src.rsplit(".", 1)[0] + ".o")
-    cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+def _compile(src: str, libdir: str = LIBDIR, extra=()) -> str:
+    obj = os.path.join(libdir, src.rsplit(".", 1)[0] + ".o")
+    cmd = [HIPCC, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -53,6 +53,24 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if verbose:
         print(f"[zonos_amd] built {LIB}", file=sys.stderr)
     return LIB
+
+
+def build_variant(name: str, defines: dict) -> str:
+    """Tuning experiments only: the same sources with -D overrides, linked into
+    lib/variants/<name>/libzonos_hip.so (select with ZK_LIB_PATH; the product uses LIB)."""
+    d = os.path.join(LIBDIR, "variants", name)
+    os.makedirs(d, exist_ok=True)
+    extra = [f"-D{k}={v}" for k, v in defines.items()]
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, d, extra), SOURCES))
+    out = os.path.join(d, "libzonos_hip.so")
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    for o in objs:
+        os.remove(o)
+    return out
 
 
 if __name__ == "__main__":

@@ -275,13 +275,20 @@ ZK_DEV void attn_step(AttnState& st, const KVFrag& f, const bf16x8* qf, int key_
 // of 128-key blocks, each wave a 32-key slice of every block, with the next slice's K/V
 // loads in flight (two register sets) while the current one is multiplied; the 4 waves merge
 // (m, l, O) through LDS at the end. nsplit == 1 writes the normalised bf16 output directly.
-__global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vt, int R,
-                                                        int H, int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
-                                                        float* work, float scale, bf16_t* out, const int32_t* skip) {
+// FUSED: the in_proj epilogue (k_qkv_rope) runs as this kernel's prologue -- each workgroup
+// reduces the split-K slabs of its own 4 query heads + 1 KV head (768 columns), applies RoPE,
+// keeps q in LDS and (the split that owns the newest key) stores the new K / V^T entries
+// before the key loop reads them. One launch per layer instead of two.
+template <bool FUSED>
+__global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H,
+                                                        int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
+                                                        float* work, float scale, bf16_t* out, const int32_t* skip,
+                                                        const float* part, int gsplit, const float* freqs) {
     constexpr int HD = 128;
     __shared__ float s_m[4][16];
     __shared__ float s_l[4][16];
     __shared__ float s_o[4][AT_G][HD];
+    __shared__ uint32_t s_q[AT_G][HD / 2];
     if (skip && *skip) return;
     const int split = blockIdx.x, nsplit = gridDim.x, g = blockIdx.y, r = blockIdx.z;
     const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
@@ -290,9 +297,49 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, const b
     const int G = H / Hkv;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ln = lane & 15, lg = lane >> 4;
+    bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
+    bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
 
     bf16x8 qf[4];
-    {
+    if constexpr (FUSED) {
+        // pairs: [0, G*64) q of heads g*G.., then 64 k pairs, then 64 v pairs
+        const int pos = ctx - 1;
+        const int N = (H + 2 * Hkv) * HD;
+        const size_t slab = (size_t)R * N;
+        const float* prow = part + (size_t)r * N;
+        const float* fc = freqs + (size_t)pos * HD;
+        const bool owner = split == nsplit - 1;        // the split whose key range holds pos
+        for (int pi = threadIdx.x; pi < (G + 2) * (HD / 2); pi += 256) {
+            int col;
+            if (pi < G * (HD / 2)) col = g * G * HD + 2 * pi;
+            else if (pi < (G + 1) * (HD / 2)) col = H * HD + g * HD + 2 * (pi - G * (HD / 2));
+            else col = (H + Hkv) * HD + g * HD + 2 * (pi - (G + 1) * (HD / 2));
+            float a = prow[col], bb = prow[col + 1];
+            for (int sl = 1; sl < gsplit; ++sl) { a += prow[sl * slab + col]; bb += prow[sl * slab + col + 1]; }
+            a = round_bf(a);
+            bb = round_bf(bb);
+            const int d = col % HD;
+            if (pi < (G + 1) * (HD / 2)) {
+                const float c = fc[d], sn = fc[d + 1];
+                const float o0 = __fsub_rn(__fmul_rn(a, c), __fmul_rn(bb, sn));
+                const float o1 = __fadd_rn(__fmul_rn(bb, c), __fmul_rn(a, sn));
+                const uint32_t pk = pack2(o0, o1);
+                if (pi < G * (HD / 2)) s_q[pi / (HD / 2)][(pi % (HD / 2))] = pk;
+                else if (owner) *reinterpret_cast<uint32_t*>(kb + (size_t)pos * HD + d) = pk;
+            } else if (owner) {
+                bf16_t* base = vb + (size_t)d * Smax + pos;
+                base[0] = f2bf(a);
+                base[Smax] = f2bf(bb);
+            }
+        }
+        __syncthreads();      // q in LDS; the new K/V stores are complete before any wave loads them
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (ln < G) v = *reinterpret_cast<const uint4*>(&s_q[ln][ks * 16 + lg * 4]);
+            qf[ks] = as_frag(v);
+        }
+    } else {
         const bf16_t* qr = q + (size_t)r * H * HD + (size_t)(g * G + ln) * HD;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -301,8 +348,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, const b
             qf[ks] = as_frag(v);
         }
     }
-    const bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
-    const bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
 
     AttnState st;
     st.m = -INFINITY;
@@ -519,10 +564,34 @@ extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt
                Smax / AT_KB);
     ZK_REQUIRE(nsplit == 1 || work != nullptr, "zk_attn_decode: nsplit > 1 needs the work buffer");
     const float scale = 1.0f / sqrtf((float)hd);
-    hipLaunchKernelGGL(k_attn_decode, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q,
-                       (const bf16_t*)k_cache, (const bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale,
-                       (bf16_t*)out, skip);
+    hipLaunchKernelGGL(k_attn_decode<false>, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work,
+                       scale, (bf16_t*)out, skip, nullptr, 0, nullptr);
     ZK_CHECK_LAUNCH("zk_attn_decode");
+    if (nsplit > 1) {
+        hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, nsplit,
+                           (bf16_t*)out, skip);
+        ZK_CHECK_LAUNCH("zk_attn_combine");
+    }
+    return 0;
+}
+
+extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
+                                  void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
+                                  const int32_t* ctx_dev, float* work, int nsplit, void* out, const int32_t* skip,
+                                  void* stream) {
+    ZK_REQUIRE(hd == 128, "zk_attn_decode_qkv: head_dim %d unsupported (128 only)", hd);
+    ZK_REQUIRE(H % Hkv == 0 && H / Hkv <= AT_G, "zk_attn_decode_qkv: GQA group %d > %d", H / Hkv, AT_G);
+    ZK_REQUIRE(Smax % AT_KB == 0, "zk_attn_decode_qkv: Smax=%d must be a multiple of %d", Smax, AT_KB);
+    ZK_REQUIRE(nsplit >= 1 && nsplit <= Smax / AT_KB, "zk_attn_decode_qkv: nsplit=%d out of [1, %d]", nsplit,
+               Smax / AT_KB);
+    ZK_REQUIRE(nsplit == 1 || work != nullptr, "zk_attn_decode_qkv: nsplit > 1 needs the work buffer");
+    ZK_REQUIRE(part != nullptr && freqs != nullptr && gemm_nsplit >= 1, "zk_attn_decode_qkv: bad arguments");
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipLaunchKernelGGL(k_attn_decode<true>, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr,
+                       (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out,
+                       skip, part, gemm_nsplit, freqs);
+    ZK_CHECK_LAUNCH("zk_attn_decode_qkv");
     if (nsplit > 1) {
         hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, nsplit,
                            (bf16_t*)out, skip);

@@ -34,6 +34,28 @@ ZK_DEV uint4 ldg_w(const bf16_t* p) {
     else return *reinterpret_cast<const uint4*>(p);
 }
 
+// Weight layout. ZK_W_PACKED: "fragment-packed" [N/16][K/32][64 lanes][8] -- the 16x32 B
+// fragment of n-tile nt and k-slice kc is one contiguous 1 KB block in lane order, and a
+// tile's K-slices follow each other, so a wave streams its 16 weight rows as ONE sequential
+// run (each wave-instruction reads 1 KB contiguous instead of 16 rows x 64 B).
+// Otherwise nn.Linear row-major [N][K].
+#ifndef ZK_W_PACKED
+#define ZK_W_PACKED 0
+#endif
+#if ZK_W_PACKED
+constexpr int WCH = 1024;     // elements per 64-wide K chunk of one wave (2 fragments)
+constexpr int WHALF = 512;
+ZK_DEV const bf16_t* w_base(const bf16_t* W, int ntile_row0, int, int K, int kbeg, int lane) {
+    return W + ((size_t)(ntile_row0 >> 4) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
+}
+#else
+constexpr int WCH = BK;
+constexpr int WHALF = 32;
+ZK_DEV const bf16_t* w_base(const bf16_t* W, int, int row, int K, int kbeg, int lane) {
+    return W + (size_t)row * K + kbeg + (lane >> 4) * 8;
+}
+#endif
+
 // LDS byte offset of 16-byte chunk c (0..7) of tile row `row` (128-byte rows, XOR swizzle)
 ZK_DEV int lds_off(int row, int c) { return row * 128 + ((c ^ (row & 7)) << 4); }
 
@@ -52,7 +74,7 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
     // this lane's weight row
     const int wn = n0 + w * 16 + ln;
     const bool wvalid = wn < N;
-    const bf16_t* wrow = W + (size_t)(wvalid ? wn : 0) * K + kbeg + lg * 8;
+    const bf16_t* wrow = w_base(W, n0 + w * 16, wvalid ? wn : 0, K, kbeg, lane);
 
     // activation staging: 4 x 16 B per thread per K chunk (row = q>>3, 16-B chunk = q&7)
     const bf16_t* arow[4];
@@ -97,8 +119,8 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
         const int pc = min(p, nchunks - 1);
-        wr0[p] = ldg_w<WNT>(wrow + pc * BK);
-        wr1[p] = ldg_w<WNT>(wrow + pc * BK + 32);
+        wr0[p] = ldg_w<WNT>(wrow + pc * WCH);
+        wr1[p] = ldg_w<WNT>(wrow + pc * WCH + WHALF);
     }
     ZK_LOAD_A(0);
     ZK_STORE_A(0);
@@ -110,8 +132,8 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
             ZK_LOAD_A(min(ch + 1, nchunks - 1));
             {
                 const int pc = min(ch + PF, nchunks - 1);
-                wr0[(u + PF) % U] = ldg_w<WNT>(wrow + pc * BK);
-                wr1[(u + PF) % U] = ldg_w<WNT>(wrow + pc * BK + 32);
+                wr0[(u + PF) % U] = ldg_w<WNT>(wrow + pc * WCH);
+                wr1[(u + PF) % U] = ldg_w<WNT>(wrow + pc * WCH + WHALF);
             }
             const char* base = smem + (ch & 1) * (BM * BK * 2);
 #pragma unroll
@@ -170,13 +192,18 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
 // (global_load_lds_dwordx4, DA chunks ahead, XOR swizzle applied on the source address), and
 // waves 0-3 only stream weights into a PF-chunk register ring; one raw s_barrier per chunk
 // publishes the next activation chunk (it does not drain VMEM).
-constexpr int WS_NB = 6;        // LDS ring slots (16 KB each)
-constexpr int WS_DA = 4;        // activation chunks in flight (loader)
+#ifndef ZK_WS_NB
+#define ZK_WS_NB 6
+#define ZK_WS_DA 4
+#define ZK_WS_OCC 1
+#endif
+constexpr int WS_NB = ZK_WS_NB;  // LDS ring slots (16 KB each)
+constexpr int WS_DA = ZK_WS_DA;  // activation chunks in flight (loader); WS_NB >= WS_DA + 2
 constexpr int WS_THREADS = 320;
-constexpr int WS_PF = 4;        // weight chunks in flight per compute wave
+constexpr int WS_PF = 4;         // weight chunks in flight per compute wave
 
 template <int MODE, int NCH, int PF>
-__global__ __launch_bounds__(WS_THREADS, 1) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
+__global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
                                                            bf16_t* __restrict__ Cout, const int32_t* skip) {
@@ -201,7 +228,11 @@ __global__ __launch_bounds__(WS_THREADS, 1) void k_gemm_ws(const bf16_t* __restr
                 const int row = 8 * i + rl;
                 const int m = min(row, M - 1);
                 const bf16_t* src = A + (size_t)m * lda + k0 + ((sl ^ (row & 7)) << 3);
+#ifndef ZK_DBG_NOALOAD
                 __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 1024), 16, 0, 0);
+#else
+                (void)src; (void)dst;
+#endif
             }
         };
         const int pre = min(WS_DA, nchunks);
@@ -222,7 +253,7 @@ __global__ __launch_bounds__(WS_THREADS, 1) void k_gemm_ws(const bf16_t* __restr
     // ---------------- compute waves
     const int wn = n0 + w * 16 + ln;
     const bool wvalid = wn < N;
-    const bf16_t* wrow = W + (size_t)(wvalid ? wn : 0) * K + kbeg + lg * 8;
+    const bf16_t* wrow = w_base(W, n0 + w * 16, wvalid ? wn : 0, K, kbeg, lane);
     f32x4 acc[8];
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -234,14 +265,14 @@ __global__ __launch_bounds__(WS_THREADS, 1) void k_gemm_ws(const bf16_t* __restr
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
         const int pc = p < NCH ? p : NCH - 1;
-        wr0[p] = ldg_w<false>(wrow + pc * BK);
-        wr1[p] = ldg_w<false>(wrow + pc * BK + 32);
+        wr0[p] = ldg_w<false>(wrow + pc * WCH);
+        wr1[p] = ldg_w<false>(wrow + pc * WCH + WHALF);
     }
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
         if (ch + PF < NCH) {
-            wr0[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * BK);
-            wr1[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * BK + 32);
+            wr0[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * WCH);
+            wr1[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * WCH + WHALF);
         }
         __builtin_amdgcn_s_barrier();                               // chunk ch is in LDS
         asm volatile("" ::: "memory");
@@ -251,8 +282,17 @@ __global__ __launch_bounds__(WS_THREADS, 1) void k_gemm_ws(const bf16_t* __restr
             const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
 #pragma unroll
             for (int mt = 0; mt < 8; ++mt) {
+#ifndef ZK_DBG_NOMFMA
                 const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
                 acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
+#else
+                if (mt == 0) {
+                    const uint4 rw = ks == 0 ? wr0[ch % U] : wr1[ch % U];
+                    acc[0][0] += __uint_as_float(rw.x ^ rw.w);
+                }
+                (void)base;
+                (void)b;
+#endif
             }
         }
     }

@@ -86,6 +86,7 @@ class HipDecoder:
     def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
         _lib.load()
         self.cfg = cfg
+        self.fuse_qkv = True      # in_proj epilogue inside the decode attention launch (False: separate kernel)
         self.device = torch.device(device)
         c = cfg
         bf = torch.bfloat16
@@ -195,11 +196,17 @@ class HipDecoder:
         for i, L in enumerate(self.layers):
             kc, vt = self._kv(ws, i)
             call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
-            call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q), ptr(kc),
-                 ptr(vt), ws["smax"], ptr(ws["vrows"]) if prefill else None, skip, stream)
             if prefill:
+                call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
+                     ptr(kc), ptr(vt), ws["smax"], ptr(ws["vrows"]), skip, stream)
                 call("zk_attn_prefill", ptr(q), ptr(kc), ptr(ws["vrows"]), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
+            elif self.fuse_qkv:
+                # in_proj epilogue fused into the attention launch (position = ctx - 1 = scal[1])
+                call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), skip, stream)
             else:
+                call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
+                     ptr(kc), ptr(vt), ws["smax"], None, skip, stream)
                 call("zk_attn_decode", ptr(q), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1, ptr(scal[1:2]),
                      ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), skip, stream)
             call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip, stream)
