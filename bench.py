@@ -51,8 +51,12 @@ def parse():
 
 
 def attn_roofline(eng, ctx, reps=50):
-    """Time the dominant kernel (split-KV decode attention) with HIP events on its stream at
-    the workload's mean context; algorithmic bytes = K+V rows read + q read + out write."""
+    """Time the dominant kernel -- the decode attention with the fused in_proj epilogue
+    (zk_attn_decode_qkv), as the generate loop launches it -- with HIP events on its stream at
+    the workload's mean context. Algorithmic bytes per launch = K+V rows read (R*ctx*Hkv*hd*2*2)
+    + in_proj slabs read (nsplit*R*(H+2Hkv)*hd*4) + out write + new K/V write. traffic: the
+    PMC-measured HBM bytes per launch of the same kernel and shape, from the committed
+    rocprofv3 summary (profiles/*attn_pmc.json, tools/attn_pmc.py), or null."""
     import ctypes as C
 
     from zonos_amd import _lib
@@ -60,28 +64,37 @@ def attn_roofline(eng, ctx, reps=50):
     ws = eng._ws
     c = eng.cfg
     R, Hk, hd, H = ws["R"], c.n_kv, c.head_dim, c.n_heads
+    gs = ws["splits"]["qkv"]
     kc, vt = eng._kv(ws, c.n_layer // 2)
     stream = _lib.stream_ptr()
     e0, e1 = _lib.P(), _lib.P()
     call("zk_event_create", C.byref(e0))
     call("zk_event_create", C.byref(e1))
-    args = (ptr(ws["q"]), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], ctx, None, ptr(ws["attn_work"]),
-            ws["attn_splits"], ptr(ws["y"]), None, stream)
+    args = (ptr(ws["part"]), gs, ptr(eng.freqs), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], ctx, None,
+            ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["y"]), None, stream)
     for _ in range(5):
-        call("zk_attn_decode", *args)
+        call("zk_attn_decode_qkv", *args)
     call("zk_event_record", e0.value, stream)
     for _ in range(reps):
-        call("zk_attn_decode", *args)
+        call("zk_attn_decode_qkv", *args)
     call("zk_event_record", e1.value, stream)
     ms = C.c_float()
     call("zk_event_elapsed_ms", e0.value, e1.value, C.byref(ms))
     call("zk_event_destroy", e0.value)
     call("zk_event_destroy", e1.value)
     per_launch_s = ms.value / 1e3 / reps
-    bytes_per_launch = R * ctx * Hk * hd * 2 * 2 + R * H * hd * 2 * 2
+    Nq = (H + 2 * Hk) * hd
+    bytes_per_launch = R * ctx * Hk * hd * 2 * 2 + gs * R * Nq * 4 + R * H * hd * 2 + R * Hk * hd * 2 * 2
     ach = bytes_per_launch / per_launch_s / 1e9
+    traffic = None
+    import glob
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*attn_pmc.json"))):
+        d = json.load(open(f))
+        if d.get("R") == R and d.get("ctx") == ctx and d.get("kernel") == "k_attn_decode<true>":
+            traffic = d["hbm_bytes_per_launch"]
     return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                traffic=None, kernel="k_attn_decode" + ("+k_attn_combine" if ws["attn_splits"] > 1 else ""),
+                traffic=traffic, kernel="k_attn_decode<true> (zk_attn_decode_qkv)" +
+                ("+k_attn_combine" if ws["attn_splits"] > 1 else ""),
                 ctx=ctx, attn_splits=ws["attn_splits"],
                 bytes_per_launch=bytes_per_launch, us_per_launch=round(per_launch_s * 1e6, 2))
 

@@ -86,11 +86,17 @@ int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, 
  * mode 0: fp32 split-K slabs Cpart[split][M][N] (nsplit = K-split count);
  * mode 1: SwiGLU epilogue for FeedForward fc1 (_torch.py:147,151-152): W rows must be
  *         in the engine's interleaved order (zk_permute_fc1) and Cout is bf16 [M][N/2].
- * lda = row stride of A in elements (lets the heads GEMM read only the last token). */
+ * lda = row stride of A in elements (lets the heads GEMM read only the last token).
+ * W is in the engine's fragment-packed layout (zk_pack_weights; rows padded to 64). */
 int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
                  float* Cpart, void* Cout, const int32_t* skip, void* stream);
 /* fc1 weight [2F][D] (rows: F "y" then F "gate") -> interleaved groups of 8 y + 8 gate rows. */
 int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream);
+/* nn.Linear weight [N][K] bf16 -> fragment-packed [ceil64(N)/16][K/32][64][8] (rows >= N zero):
+ * each 16x32 MFMA B fragment is one contiguous 1 KB block in lane order, a 16-row tile's
+ * K-slices consecutive, so every wave streams its weights as one sequential run.
+ * out holds ceil64(N)*K elements. K % 64 == 0. */
+int zk_pack_weights(const void* w, int N, int K, void* out, void* stream);
 
 /* Sum split-K slabs of in_proj, round to bf16, apply interleaved RoPE to q and k
  * (apply_rotary_emb _torch.py:18-30; positions pos0 + t (+ *pos_dev if non-NULL);

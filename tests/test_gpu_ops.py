@@ -81,12 +81,31 @@ def test_gemm_vs_fp32(M, N, K, nsplit):
     g = torch.Generator(device="cpu").manual_seed(M + N)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
     W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    from zonos_amd.engine import pack_weights
+    Wpk = pack_weights(W, stream_ptr())
     part = torch.empty(nsplit, M, N, device=DEV)
-    call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, nsplit, 0, ptr(part), None, None, stream_ptr())
+    call("zk_gemm_bf16", ptr(A), K, ptr(Wpk), M, N, K, nsplit, 0, ptr(part), None, None, stream_ptr())
     got = part.sum(0)
     ref = A.float() @ W.float().t()
     # fp32 accumulation of bf16 products: error ~ K * eps32 * |a||w|
     assert torch.allclose(got, ref, atol=2e-3 * (K / 2048) ** 0.5, rtol=1e-3), (got - ref).abs().max()
+
+
+def test_pack_weights_layout():
+    """Fragment-packed layout: block (nt, kc) lane l holds W[16nt + l%16][32kc + 8(l//16) .. +8]."""
+    from zonos_amd._lib import stream_ptr
+    from zonos_amd.engine import pack_weights
+    N, K = 100, 128
+    W = torch.arange(N * K, dtype=torch.float32).reshape(N, K).to(torch.bfloat16).to(DEV)
+    P = pack_weights(W, stream_ptr()).cpu().reshape(-1, K // 32, 64, 8)
+    assert P.shape[0] == 128 // 16
+    Wc = W.cpu()
+    for nt in range(P.shape[0]):
+        for kc in range(K // 32):
+            for lane in (0, 5, 17, 63):
+                n, k = nt * 16 + lane % 16, kc * 32 + 8 * (lane // 16)
+                exp = Wc[n, k:k + 8] if n < N else torch.zeros(8, dtype=torch.bfloat16)
+                assert torch.equal(P[nt, kc, lane], exp)
 
 
 def test_gemm_swiglu():
@@ -100,6 +119,8 @@ def test_gemm_swiglu():
     Wp = torch.empty_like(W1).to(DEV)
     s = stream_ptr()
     call("zk_permute_fc1", ptr(W1.to(DEV)), Fd, D, ptr(Wp), s)
+    from zonos_amd.engine import pack_weights
+    Wp = pack_weights(Wp, s)
     A_d = A.to(DEV)
     out = torch.empty(M, Fd, dtype=torch.bfloat16, device=DEV)
     call("zk_gemm_bf16", ptr(A_d), D, ptr(Wp), M, 2 * Fd, D, 1, 1, None, ptr(out), None, s)

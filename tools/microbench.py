@@ -38,7 +38,7 @@ def gemm():
         # distinct weight buffers per rep set so L2/MALL does not serve them: rotate 8 copies (>256 MB total)
         ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
         Npad = (N + 63) // 64 * 64        # packed layout reads whole 64-row tiles
-        Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]   # packed-size buffers
         A = torch.randn(M, K, device=dev).to(torch.bfloat16)
         ns = 1 if mode == 1 else _split_for(N, K, M, int(os.environ.get("ZK_SPLIT_TARGET", "256")))
         part = torch.empty(ns * M * N, device=dev)

@@ -1,0 +1,45 @@
+"""Summarise rocprofv3 --pmc CSV output: mean counter value per (kernel, grid) over dispatches.
+FETCH_SIZE is reported x2 (gfx950 counts wide streaming reads at half: MI355X_MICROARCH.md).
+
+    python tools/pmc_summary.py DIR [DIR ...] [--json OUT --match NAME --R 128 --ctx 1705 --alg BYTES]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+ap = argparse.ArgumentParser()
+ap.add_argument("dirs", nargs="+")
+ap.add_argument("--json")
+ap.add_argument("--match", default="k_attn_decode<true>")
+ap.add_argument("--R", type=int, default=128)
+ap.add_argument("--ctx", type=int, default=1705)
+ap.add_argument("--alg", type=float, default=0)
+a = ap.parse_args()
+
+acc = defaultdict(list)
+for d in a.dirs:
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r.get("Kernel_Name", "?")
+            acc[(name, r.get("Grid_Size", "?"), r["Counter_Name"])].append(float(r["Counter_Value"]))
+per = {}
+for (name, grid, cn), v in sorted(acc.items()):
+    mean = sum(v) / len(v)
+    corr = 2 if cn == "FETCH_SIZE" else 1
+    mb = mean * 1024 * corr / 1e6
+    short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][-60:]
+    print(f"{short:60s} grid={grid:>8s} {cn:10s} n={len(v):4d} mean={mean:12.1f} KB "
+          f"-> {mb:10.2f} MB/launch{' (x2 gfx950)' if corr == 2 else ''}")
+    if a.match in name:
+        per[cn] = max(per.get(cn, 0.0), mean * 1024 * corr)
+if a.json and per:
+    tot = per.get("FETCH_SIZE", 0.0) + per.get("WRITE_SIZE", 0.0)
+    out = dict(kernel=a.match, R=a.R, ctx=a.ctx, fetch_bytes=per.get("FETCH_SIZE"), write_bytes=per.get("WRITE_SIZE"),
+               hbm_bytes_per_launch=tot, algorithmic_bytes_per_launch=a.alg,
+               ratio=(tot / a.alg if a.alg else None),
+               method="rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH_SIZE x2 (gfx950)")
+    json.dump(out, open(a.json, "w"), indent=1)
+    print(json.dumps(out))

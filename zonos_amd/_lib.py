@@ -47,6 +47,7 @@ _SIGS = {
     "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, P, P],
     "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
     "zk_permute_fc1": [P, I, I, P, P],
+    "zk_pack_weights": [P, I, I, P, P],
     "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, P, P],
     "zk_attn_decode": [P, P, P, I, I, I, I, I, I, P, P, I, P, P, P],
     "zk_attn_decode_qkv": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, P, P, P],

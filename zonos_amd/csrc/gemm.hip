@@ -40,7 +40,7 @@ ZK_DEV uint4 ldg_w(const bf16_t* p) {
 // run (each wave-instruction reads 1 KB contiguous instead of 16 rows x 64 B).
 // Otherwise nn.Linear row-major [N][K].
 #ifndef ZK_W_PACKED
-#define ZK_W_PACKED 0
+#define ZK_W_PACKED 1
 #endif
 #if ZK_W_PACKED
 constexpr int WCH = 1024;     // elements per 64-wide K chunk of one wave (2 fragments)
@@ -325,6 +325,21 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
     }
 }
 
+// nn.Linear [N][K] -> fragment-packed [Npad/16][K/32][64][8] (rows >= N zero)
+__global__ void k_pack_w(const bf16_t* __restrict__ w, int N, int K, int Npad, bf16_t* __restrict__ out) {
+    const size_t total = (size_t)Npad / 16 * (K / 32) * 64;      // 16-byte pieces
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(i & 63);
+        const size_t frag = i >> 6;
+        const int kc = (int)(frag % (K / 32));
+        const int nt = (int)(frag / (K / 32));
+        const int n = nt * 16 + (lane & 15), k = kc * 32 + (lane >> 4) * 8;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (n < N) v = *reinterpret_cast<const uint4*>(w + (size_t)n * K + k);
+        *reinterpret_cast<uint4*>(out + i * 8) = v;
+    }
+}
+
 __global__ void k_permute_fc1(const bf16_t* w, int F, int D, bf16_t* out) {
     const int nr = blockIdx.x;         // new row
     const int q = nr / 16, j = nr % 16;
@@ -335,6 +350,17 @@ __global__ void k_permute_fc1(const bf16_t* w, int F, int D, bf16_t* out) {
 }
 
 }  // namespace
+
+extern "C" int zk_pack_weights(const void* w, int N, int K, void* out, void* stream) {
+    ZK_REQUIRE(N > 0 && K > 0 && K % 64 == 0, "zk_pack_weights: N=%d K=%d (K %% 64 != 0)", N, K);
+    const int Npad = (N + 63) / 64 * 64;
+    const size_t total = (size_t)Npad / 16 * (K / 32) * 64;
+    const int grid = (int)std::min<size_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_pack_w, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)w, N, K, Npad,
+                       (bf16_t*)out);
+    ZK_CHECK_LAUNCH("zk_pack_weights");
+    return 0;
+}
 
 extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
                             float* Cpart, void* Cout, const int32_t* skip_flag, void* stream) {

@@ -59,6 +59,14 @@ def rope_table(seq_len: int, head_dim: int, base: float = 10000.0) -> torch.Tens
     return torch.stack([z.real, z.imag], dim=-1).contiguous()
 
 
+def pack_weights(w: torch.Tensor, stream) -> torch.Tensor:
+    """nn.Linear bf16 [N][K] -> the GEMM's fragment-packed layout (zk_pack_weights)."""
+    N, K = w.shape
+    out = torch.empty((N + 63) // 64 * 64, K, dtype=w.dtype, device=w.device)
+    call("zk_pack_weights", ptr(w), N, K, ptr(out), stream)
+    return out
+
+
 def _split_for(N: int, K: int, M: int, target_blocks: int = 256) -> int:
     """Split-K count for the 128x64-tile GEMM: enough workgroups to cover the CUs.
     Depends on (N, K) only for M <= 128 so the reduction order is batch-invariant."""
@@ -104,19 +112,21 @@ class HipDecoder:
             if h.shape[0] < VOCAB:      # pad_weight_ (utils.py:22-37): 1025 -> 1026 rows
                 h = torch.cat([h, h.new_zeros(VOCAB - h.shape[0], h.shape[1])])
             heads.append(h)
-        self.heads = torch.cat(heads).contiguous()          # [9*1026][D]
-        self.layers = []
         stream = _lib.stream_ptr(dev)
+        self.heads = pack_weights(torch.cat(heads).contiguous(), stream)    # [9*1026 -> 9280][D] packed
+        self.layers = []
         for i in range(c.n_layer):
             p = f"backbone.layers.{i}."
             fc1 = w(p + "mlp.fc1.weight")
             fc1p = torch.empty_like(fc1)
             call("zk_permute_fc1", ptr(fc1), c.d_ff, c.d_model, ptr(fc1p), stream)
+            del fc1
             self.layers.append(dict(
                 ln1_w=w(p + "norm.weight"), ln1_b=w(p + "norm.bias"),
-                wqkv=w(p + "mixer.in_proj.weight"), wo=w(p + "mixer.out_proj.weight"),
+                wqkv=pack_weights(w(p + "mixer.in_proj.weight"), stream),
+                wo=pack_weights(w(p + "mixer.out_proj.weight"), stream),
                 ln2_w=w(p + "norm2.weight"), ln2_b=w(p + "norm2.bias"),
-                fc1=fc1p, fc2=w(p + "mlp.fc2.weight")))
+                fc1=pack_weights(fc1p, stream), fc2=pack_weights(w(p + "mlp.fc2.weight"), stream)))
         self.lnf_w = w("backbone.norm_f.weight")
         self.lnf_b = w("backbone.norm_f.bias")
         self.freqs = rope_table(16384, c.head_dim).to(dev)
