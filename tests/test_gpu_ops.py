@@ -186,6 +186,42 @@ def test_attention_decode(R, ctx, H, Hk, nsplit):
     assert (out.float().cpu() - ref).abs().max() < 2e-2
 
 
+@pytest.mark.parametrize("R,ctx,H,Hk,nsplit,gs", [(4, 1, 16, 4, 1, 4), (6, 37, 2, 1, 2, 2), (128, 300, 16, 4, 1, 4),
+                                                   (3, 700, 16, 4, 4, 8), (2, 129, 2, 1, 1, 1), (5, 256, 16, 4, 2, 3)])
+def test_attention_decode_fused_qkv_equals_separate(R, ctx, H, Hk, nsplit, gs):
+    """zk_attn_decode_qkv == zk_qkv_rope (at pos = ctx-1) + zk_attn_decode: bit-identical
+    output and identical cache contents afterwards."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import rope_table
+    hd = 128
+    smax = ((ctx + 255) // 256) * 256
+    nsplit = min(nsplit, smax // 128)
+    g = torch.Generator(device="cpu").manual_seed(R * 1000 + ctx)
+    N = (H + 2 * Hk) * hd
+    part = (torch.randn(gs, R, N, generator=g) * 0.5).to(DEV)
+    kc0 = torch.randn(R * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    vt0 = torch.randn(R * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    freqs = rope_table(16384, hd).to(DEV)
+    s = stream_ptr()
+    work = torch.empty(R * Hk * nsplit * (8 + 4 * hd), device=DEV)
+    # separate kernels
+    kc1, vt1 = kc0.clone(), vt0.clone()
+    q = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
+    out1 = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
+    call("zk_qkv_rope", ptr(part), gs, R, 1, H, Hk, hd, ptr(freqs), ctx - 1, None, ptr(q), ptr(kc1), ptr(vt1), smax,
+         None, None, s)
+    call("zk_attn_decode", ptr(q), ptr(kc1), ptr(vt1), R, H, Hk, hd, smax, ctx, None, ptr(work), nsplit, ptr(out1),
+         None, s)
+    # fused
+    kc2, vt2 = kc0.clone(), vt0.clone()
+    out2 = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
+    call("zk_attn_decode_qkv", ptr(part), gs, ptr(freqs), ptr(kc2), ptr(vt2), R, H, Hk, hd, smax, ctx, None,
+         ptr(work), nsplit, ptr(out2), None, s)
+    torch.cuda.synchronize()
+    assert torch.equal(kc1, kc2) and torch.equal(vt1, vt2)
+    assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max()
+
+
 @pytest.mark.parametrize("R,S,H,Hk", [(2, 1, 2, 1), (3, 70, 16, 4), (2, 200, 2, 1)])
 def test_attention_prefill(R, S, H, Hk):
     from zonos_amd._lib import call, ptr, stream_ptr

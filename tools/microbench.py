@@ -64,9 +64,33 @@ def attn():
         kcs = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
         vts = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
         q = torch.randn(R, H * hd, device=dev).to(torch.bfloat16)
-        from zonos_amd.engine import attn_splits_for
-        for ms_ in sorted({attn_splits_for(R, Hk, smax), 1, 4}):
+        from zonos_amd.engine import attn_splits_for, rope_table
+        for ms_ in sorted({attn_splits_for(R, Hk, smax), 1}):
             attn_one(R, H, Hk, hd, ctx, smax, kcs, vts, q, ms_, ncopy)
+        # fused in_proj epilogue (the product path)
+        gs = 4
+        part = torch.randn(gs * R * (H + 2 * Hk) * hd, device=dev) * 0.1
+        freqs = rope_table(16384, hd).to(dev)
+        work = torch.empty(R * Hk * (8 + 4 * hd), device=dev)
+        out = torch.empty(R, H * hd, dtype=torch.bfloat16, device=dev)
+        it = [0]
+
+        def fq():
+            i = it[0] % ncopy
+            it[0] += 1
+            call("zk_attn_decode_qkv", ptr(part), gs, ptr(freqs), ptr(kcs[i]), ptr(vts[i]), R, H, Hk, hd, smax, ctx,
+                 None, ptr(work), 1, ptr(out), None, S)
+        us = timeit(fq)
+        b = R * ctx * Hk * hd * 2 * 2 + gs * R * (H + 2 * Hk) * hd * 4
+        print(f"attn+qkv ctx={ctx:5d} fused: {us:8.1f} us  {b/1e6:7.1f} MB  {b / (us * 1e-6) / 1e9:7.0f} GB/s",
+              flush=True)
+        qkv_out = torch.empty(R, H * hd, dtype=torch.bfloat16, device=dev)
+
+        def fr():
+            call("zk_qkv_rope", ptr(part), gs, R, 1, H, Hk, hd, ptr(freqs), ctx - 1, None, ptr(qkv_out), ptr(kcs[0]),
+                 ptr(vts[0]), smax, None, None, S)
+        us = timeit(fr)
+        print(f"qkv_rope alone ctx={ctx:5d}: {us:8.1f} us", flush=True)
 
 
 def attn_one(R, H, Hk, hd, ctx, smax, kcs, vts, q, ms_, ncopy):

@@ -19,7 +19,10 @@ LIB = os.path.join(LIBDIR, "libzonos_hip.so")
 SOURCES = ["sampler.hip", "backbone.hip", "gemm.hip", "dac.hip", "dac_mfma.hip", "dac_cl.hip", "capi.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+# -ffp-contract=off: no implicit FMA contraction -- the reference rounds every elementwise op
+# (torch CPU kernels are unfused) and __fmul_rn / __fadd_rn are plain operators in HIP, so
+# contraction would make results depend on how each kernel happens to be scheduled.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", "-ffp-contract=off"]
 
 
 def _deps_mtime() -> float:

@@ -195,6 +195,7 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit,
 constexpr int AT_KB = 128;      // keys per workgroup iteration (4 waves x 32)
 constexpr int AT_G = 4;         // query heads per KV head handled by the B operand (<= 16)
 constexpr int AT_STR = 2 * AT_G + AT_G * 128;   // work floats per (r, g, split)
+constexpr int AT_MAXGS = 8;     // max in_proj split-K slabs the fused prologue reduces
 
 // One 32-key step of one wave: registers for K (A operand of S^T = K.Q^T) and V^T
 // (A operand of O^T = V^T.P^T). Key mapping inside the 32: MFMA row r = 4*grp + i of tile h
@@ -275,6 +276,30 @@ ZK_DEV void attn_step(AttnState& st, const KVFrag& f, const bf16x8* qf, int key_
 // of 128-key blocks, each wave a 32-key slice of every block, with the next slice's K/V
 // loads in flight (two register sets) while the current one is multiplied; the 4 waves merge
 // (m, l, O) through LDS at the end. nsplit == 1 writes the normalised bf16 output directly.
+// Replace the newest key's K row / V^T entries in a loaded 32-key slice by the values kept in
+// LDS (their cache lines are written at the end of the fused kernel). Wave-uniform early out.
+ZK_DEV void patch_kv(KVFrag& f, const uint32_t* s_kn, const uint16_t* s_vn, int key_base, int pos, int ln, int lg) {
+    if (pos < key_base || pos >= key_base + 32) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int key = key_base + 8 * (ln >> 2) + 4 * h + (ln & 3);
+        if (key == pos) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = *reinterpret_cast<const uint4*>(s_kn + ks * 16 + lg * 4);
+        }
+    }
+    const int e = pos - key_base - 8 * lg;      // element of this lane's 8-key V^T group
+    if (e >= 0 && e < 8) {
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            uint16_t tmp[8];
+            *reinterpret_cast<uint4*>(tmp) = f.v[dt];
+            tmp[e] = s_vn[dt * 16 + ln];
+            f.v[dt] = *reinterpret_cast<const uint4*>(tmp);
+        }
+    }
+}
+
 // FUSED: the in_proj epilogue (k_qkv_rope) runs as this kernel's prologue -- each workgroup
 // reduces the split-K slabs of its own 4 query heads + 1 KV head (768 columns), applies RoPE,
 // keeps q in LDS and (the split that owns the newest key) stores the new K / V^T entries
@@ -288,7 +313,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     __shared__ float s_m[4][16];
     __shared__ float s_l[4][16];
     __shared__ float s_o[4][AT_G][HD];
-    __shared__ uint32_t s_q[AT_G][HD / 2];
+    __shared__ __attribute__((aligned(16))) uint32_t s_q[AT_G][HD / 2];
+    __shared__ __attribute__((aligned(16))) uint32_t s_kn[HD / 2];   // new key (post-RoPE), bf16 pairs
+    __shared__ uint16_t s_vn[HD];                                    // new value
     if (skip && *skip) return;
     const int split = blockIdx.x, nsplit = gridDim.x, g = blockIdx.y, r = blockIdx.z;
     const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
@@ -301,38 +328,59 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
 
     bf16x8 qf[4];
+    KVFrag fa, fb;
+    const int last = kb1 - 1;
+    // the first key block can be fetched before the prologue unless it holds the new key
+    // FUSED: the new key's cache lines are written only at the end of the kernel (a store
+    // followed by loads of the same partially written lines stalls the key loop); the key loop
+    // patches the new K/V into its registers from LDS instead, so the arithmetic is exactly
+    // that of reading the cache. The first key block can therefore be fetched before the prologue.
+    const int pos = ctx - 1;
+    const bool early = FUSED && kb1 > kb0;
+    if (early) load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
     if constexpr (FUSED) {
         // pairs: [0, G*64) q of heads g*G.., then 64 k pairs, then 64 v pairs
-        const int pos = ctx - 1;
         const int N = (H + 2 * Hkv) * HD;
         const size_t slab = (size_t)R * N;
         const float* prow = part + (size_t)r * N;
         const float* fc = freqs + (size_t)pos * HD;
-        const bool owner = split == nsplit - 1;        // the split whose key range holds pos
         for (int pi = threadIdx.x; pi < (G + 2) * (HD / 2); pi += 256) {
             int col;
             if (pi < G * (HD / 2)) col = g * G * HD + 2 * pi;
             else if (pi < (G + 1) * (HD / 2)) col = H * HD + g * HD + 2 * (pi - G * (HD / 2));
             else col = (H + Hkv) * HD + g * HD + 2 * (pi - (G + 1) * (HD / 2));
-            float a = prow[col], bb = prow[col + 1];
-            for (int sl = 1; sl < gsplit; ++sl) { a += prow[sl * slab + col]; bb += prow[sl * slab + col + 1]; }
+            // all slab loads issued together (clamped slab index, select after) -- same
+            // left-to-right fp32 sum as k_qkv_rope
+            float2 v[AT_MAXGS];
+#pragma unroll
+            for (int sl = 0; sl < AT_MAXGS; ++sl)
+                v[sl] = *reinterpret_cast<const float2*>(prow + (size_t)min(sl, gsplit - 1) * slab + col);
+            const int d = col % HD;
+            const float2 cs = *reinterpret_cast<const float2*>(fc + d);
+            float a = v[0].x, bb = v[0].y;
+#pragma unroll
+            for (int sl = 1; sl < AT_MAXGS; ++sl)
+                if (sl < gsplit) { a += v[sl].x; bb += v[sl].y; }
             a = round_bf(a);
             bb = round_bf(bb);
-            const int d = col % HD;
             if (pi < (G + 1) * (HD / 2)) {
-                const float c = fc[d], sn = fc[d + 1];
-                const float o0 = __fsub_rn(__fmul_rn(a, c), __fmul_rn(bb, sn));
-                const float o1 = __fadd_rn(__fmul_rn(bb, c), __fmul_rn(a, sn));
+                const float o0 = __fsub_rn(__fmul_rn(a, cs.x), __fmul_rn(bb, cs.y));
+                const float o1 = __fadd_rn(__fmul_rn(bb, cs.x), __fmul_rn(a, cs.y));
                 const uint32_t pk = pack2(o0, o1);
                 if (pi < G * (HD / 2)) s_q[pi / (HD / 2)][(pi % (HD / 2))] = pk;
-                else if (owner) *reinterpret_cast<uint32_t*>(kb + (size_t)pos * HD + d) = pk;
-            } else if (owner) {
-                bf16_t* base = vb + (size_t)d * Smax + pos;
-                base[0] = f2bf(a);
-                base[Smax] = f2bf(bb);
+                else s_kn[d / 2] = pk;
+            } else {
+                s_vn[d] = f2bf(a);
+                s_vn[d + 1] = f2bf(bb);
             }
         }
-        __syncthreads();      // q in LDS; the new K/V stores are complete before any wave loads them
+        __syncthreads();      // q, new k, new v in LDS
+#ifdef ZK_ATT_DBGQ
+        if (q != nullptr && split == 0)
+            for (int i = threadIdx.x; i < G * HD / 2; i += 256)
+                reinterpret_cast<uint32_t*>(const_cast<bf16_t*>(q))[((size_t)r * H + g * G) * (HD / 2) + i] =
+                    s_q[i / (HD / 2)][i % (HD / 2)];
+#endif
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             uint4 v = make_uint4(0, 0, 0, 0);
@@ -348,7 +396,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
             qf[ks] = as_frag(v);
         }
     }
-
     AttnState st;
     st.m = -INFINITY;
     st.l = 0.f;
@@ -356,15 +403,22 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if (kb1 > kb0) {
-        KVFrag fa, fb;
-        const int last = kb1 - 1;
-        load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
+        if (!early) load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         for (int it = kb0; it < kb1; it += 2) {
             load_kv(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
+            if (FUSED) patch_kv(fa, s_kn, s_vn, it * AT_KB + 32 * w, pos, ln, lg);
             attn_step(st, fa, qf, it * AT_KB + 32 * w, ctx, scale, lg);
             load_kv(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
-            if (it + 1 < kb1) attn_step(st, fb, qf, (it + 1) * AT_KB + 32 * w, ctx, scale, lg);
+            if (it + 1 < kb1) {
+                if (FUSED) patch_kv(fb, s_kn, s_vn, (it + 1) * AT_KB + 32 * w, pos, ln, lg);
+                attn_step(st, fb, qf, (it + 1) * AT_KB + 32 * w, ctx, scale, lg);
+            }
         }
+    }
+    if (FUSED && split == nsplit - 1) {      // the split owning the newest key stores it (cache for later steps)
+        const int t = threadIdx.x;
+        if (t < HD / 2) *reinterpret_cast<uint32_t*>(kb + (size_t)pos * HD + 2 * t) = s_kn[t];
+        else if (t < HD / 2 + HD) reinterpret_cast<uint16_t*>(vb)[(size_t)(t - HD / 2) * Smax + pos] = s_vn[t - HD / 2];
     }
     // merge the 4 waves
     if (lg == 0) { s_m[w][ln] = st.m; s_l[w][ln] = st.l; }
@@ -586,9 +640,15 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
     ZK_REQUIRE(nsplit >= 1 && nsplit <= Smax / AT_KB, "zk_attn_decode_qkv: nsplit=%d out of [1, %d]", nsplit,
                Smax / AT_KB);
     ZK_REQUIRE(nsplit == 1 || work != nullptr, "zk_attn_decode_qkv: nsplit > 1 needs the work buffer");
-    ZK_REQUIRE(part != nullptr && freqs != nullptr && gemm_nsplit >= 1, "zk_attn_decode_qkv: bad arguments");
+    ZK_REQUIRE(part != nullptr && freqs != nullptr && gemm_nsplit >= 1 && gemm_nsplit <= AT_MAXGS,
+               "zk_attn_decode_qkv: bad arguments (gemm_nsplit=%d, max %d)", gemm_nsplit, AT_MAXGS);
     const float scale = 1.0f / sqrtf((float)hd);
-    hipLaunchKernelGGL(k_attn_decode<true>, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr,
+#ifdef ZK_ATT_DBGQ
+    const bf16_t* dbgq = (const bf16_t*)work;
+#else
+    const bf16_t* dbgq = nullptr;
+#endif
+    hipLaunchKernelGGL(k_attn_decode<true>, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq,
                        (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out,
                        skip, part, gemm_nsplit, freqs);
     ZK_CHECK_LAUNCH("zk_attn_decode_qkv");
