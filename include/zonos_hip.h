@@ -102,7 +102,9 @@ int zk_pack_weights(const void* w, int N, int K, void* out, void* stream);
  * (apply_rotary_emb _torch.py:18-30; positions pos0 + t (+ *pos_dev if non-NULL);
  * freqs = precompute_freqs_cis table [16384][hd/2][2], _torch.py:9-15), store q
  * [rows][H*hd] and write k, v into the layer cache (_update_kv_cache _torch.py:33-49).
- * Cache layout (engine-owned): K [R][Hkv][Smax][hd], V^T [R][Hkv][hd][Smax].
+ * Cache layout (engine-owned; hd = 128): per (row, kv head) Smax keys in 32-key slices of
+ * 8 KB stored in MFMA-fragment order (backbone.hip k_off / v_off; zonos_amd.kvlayout):
+ *   K: [R][Hkv][Smax/32][h 2][ks 4][lane 64][8],  V: [R][Hkv][Smax/32][dt 8][lane 64][8].
  * v_rows (nullable): also write V as [R][Hkv][S][hd] (prefill scratch).
  * rows = R*S tokens ordered r*S + t. */
 int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv, int hd,

@@ -57,3 +57,24 @@ def test_split_selection_batch_invariant():
         assert K % (s * 64) == 0
         assert all(_split_for(N, K, m) == s for m in (2, 8, 64, 128))
         assert ((N + 63) // 64) * s >= 128
+
+
+def test_kv_layout_pack_roundtrip():
+    """zonos_amd.kvlayout (host view of backbone.hip k_off / v_off): pack/unpack are inverse
+    and element positions follow the documented fragment order."""
+    import torch
+    from zonos_amd.kvlayout import pack_k, pack_v, unpack_k, unpack_v
+    R, Hk, S = 2, 3, 64
+    k, v = torch.randn(R, Hk, S, 128), torch.randn(R, Hk, S, 128)
+    kp, vp = pack_k(k), pack_v(v)
+    assert torch.equal(unpack_k(kp, S), k) and torch.equal(unpack_v(vp, S), v)
+    for key in (0, 5, 13, 31, 37, 63):
+        o = key & 31
+        ln = 4 * (o >> 3) + (o & 3)
+        h = (o >> 2) & 1
+        for c8 in (0, 3, 7, 15):
+            off = (key >> 5) * 4096 + ((h * 4 + (c8 >> 2)) * 64 + (c8 & 3) * 16 + ln) * 8
+            assert torch.equal(kp[1, 2, off:off + 8], k[1, 2, key, 8 * c8:8 * c8 + 8])
+        for ch in (0, 17, 127):
+            off = (key >> 5) * 4096 + ((ch >> 4) * 64 + (o >> 3) * 16 + (ch & 15)) * 8 + (o & 7)
+            assert vp[1, 2, off] == v[1, 2, key, ch]

@@ -158,11 +158,12 @@ def _attn_setup(R, S_ctx, H, Hk, hd, smax, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     k = torch.randn(R, S_ctx, Hk, hd, generator=g).to(torch.bfloat16)
     v = torch.randn(R, S_ctx, Hk, hd, generator=g).to(torch.bfloat16)
-    kc = torch.zeros(R, Hk, smax, hd, dtype=torch.bfloat16)
-    vt = torch.zeros(R, Hk, hd, smax, dtype=torch.bfloat16)
-    kc[:, :, :S_ctx] = k.transpose(1, 2)
-    vt[:, :, :, :S_ctx] = v.permute(0, 2, 3, 1)
-    return k, v, kc, vt
+    from zonos_amd.kvlayout import pack_k, pack_v
+    kf = torch.zeros(R, Hk, smax, hd, dtype=torch.bfloat16)
+    vf = torch.zeros(R, Hk, smax, hd, dtype=torch.bfloat16)
+    kf[:, :, :S_ctx] = k.transpose(1, 2)
+    vf[:, :, :S_ctx] = v.transpose(1, 2)
+    return k, v, pack_k(kf), pack_v(vf)
 
 
 @pytest.mark.parametrize("R,ctx,H,Hk,nsplit", [(4, 1, 16, 4, 1), (3, 300, 16, 4, 2), (2, 1000, 2, 1, 8),
@@ -254,16 +255,19 @@ def test_qkv_rope_matches_oracle():
     q_ref = zonos_ref.rope(qr.reshape(R, S, H, hd), fc).reshape(R * S, H * hd)
     k_ref = zonos_ref.rope(kr.reshape(R, S, Hk, hd), fc)
     q = torch.empty(R * S, H * hd, dtype=torch.bfloat16, device=DEV)
-    kc = torch.zeros(R, Hk, smax, hd, dtype=torch.bfloat16, device=DEV)
-    vt = torch.zeros(R, Hk, hd, smax, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(R, Hk, smax * hd, dtype=torch.bfloat16, device=DEV)
+    vt = torch.zeros(R, Hk, smax * hd, dtype=torch.bfloat16, device=DEV)
     vrows = torch.zeros(R, Hk, S, hd, dtype=torch.bfloat16, device=DEV)
     pd, fd = part.to(DEV), fr.to(DEV)
     call("zk_qkv_rope", ptr(pd), 2, R, S, H, Hk, hd, ptr(fd), pos0, None, ptr(q), ptr(kc), ptr(vt), smax, ptr(vrows),
          None, stream_ptr())
     # slab sums in a different order can flip one bf16 rounding; then RoPE is exact fp32
     assert (q.float().cpu() - q_ref.float()).abs().max() < 0.05
-    assert (kc[:, :, pos0:pos0 + S].transpose(1, 2).float().cpu() - k_ref.float()).abs().max() < 0.05
-    assert torch.equal(vt[:, :, :, pos0:pos0 + S].permute(0, 3, 1, 2).cpu(), vr.reshape(R, S, Hk, hd))
+    from zonos_amd.kvlayout import unpack_k, unpack_v
+    kk, vv = unpack_k(kc.cpu(), smax), unpack_v(vt.cpu(), smax)
+    assert (kk[:, :, pos0:pos0 + S].transpose(1, 2).float() - k_ref.float()).abs().max() < 0.05
+    assert torch.equal(vv[:, :, pos0:pos0 + S].transpose(1, 2), vr.reshape(R, S, Hk, hd))
+    assert kk[:, :, :pos0].abs().sum() == 0 and vv[:, :, pos0 + S:].abs().sum() == 0
     assert torch.equal(vrows.permute(0, 2, 1, 3).cpu(), vr.reshape(R, S, Hk, hd))
 
 

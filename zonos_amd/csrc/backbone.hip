@@ -25,6 +25,25 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 ZK_DEV bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
+// ------------------------------------------------------------------ KV cache layout
+// Per (row, kv head) the cache holds Smax keys in 32-key slices of 8 KB. Inside a slice the
+// data is stored in exactly the order the decode wave's MFMA fragments consume it, so every
+// fragment load is one contiguous 1 KB read:
+//   K: [slice][h 2][ks 4][lane 64][8]  lane = 16*lg + ln holds key 8*(ln>>2) + 4h + (ln&3)
+//      of the slice, dims 32ks + 8lg .. +8          (A operand of S^T = K.Q^T)
+//   V: [slice][dt 8][lane 64][8]       lane holds channel 16dt + ln, keys 8lg .. 8lg+7
+//                                                  (A operand of O^T = V^T.P^T)
+// Element offsets within one (row, kv head) block of Smax*128 elements:
+ZK_DEV size_t k_off(int key, int c8) {      // dims 8*c8 .. 8*c8+7 of key
+    const int o = key & 31, grp = o >> 3, h = (o >> 2) & 1, i = o & 3;
+    const int ln = 4 * grp + i, ks = c8 >> 2, lg = c8 & 3;
+    return (size_t)(key >> 5) * 4096 + ((h * 4 + ks) * 64 + lg * 16 + ln) * 8;
+}
+ZK_DEV size_t v_off(int key, int ch) {      // channel ch of key
+    const int o = key & 31, lg = o >> 3, e = o & 7;
+    return (size_t)(key >> 5) * 4096 + ((ch >> 4) * 64 + lg * 16 + (ch & 15)) * 8 + e;
+}
+
 // ------------------------------------------------------------------ LayerNorm helper
 // Row of D elements, 8 per thread (D = 8 * NT * n8). Two-pass mean/var in fp32,
 // y = (x - mean) * rstd * w + b rounded to bf16 (nn.LayerNorm, eps from config).
@@ -175,14 +194,14 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit,
                 *reinterpret_cast<uint32_t*>(q_out + (size_t)row * H * hd + col) = pk;
             } else {
                 const int g = (col - H * hd) / hd;
-                *reinterpret_cast<uint32_t*>(kc + (((size_t)r * Hkv + g) * Smax + pos) * hd + d) = pk;
+                *reinterpret_cast<uint32_t*>(kc + ((size_t)r * Hkv + g) * Smax * hd + k_off(pos, d >> 3) + (d & 7)) = pk;
             }
         } else {
             const int g = (col - (H + Hkv) * hd) / hd;
-            bf16_t* base = vt + (((size_t)r * Hkv + g) * hd + d) * Smax + pos;
+            bf16_t* base = vt + ((size_t)r * Hkv + g) * Smax * hd;
             const bf16_t va = f2bf(a), vb = f2bf(bb);
-            base[0] = va;
-            base[Smax] = vb;
+            base[v_off(pos, d)] = va;
+            base[v_off(pos, d + 1)] = vb;
             if (v_rows) {
                 *reinterpret_cast<uint32_t*>(v_rows + (((size_t)r * Hkv + g) * S + t) * hd + d) =
                     (uint32_t)va | ((uint32_t)vb << 16);
@@ -207,16 +226,16 @@ struct KVFrag {
 };
 
 ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int key_base, int ln, int lg) {
+    (void)Smax;
+    const int lane = lg * 16 + ln;
+    const bf16_t* k0 = kb + (size_t)(key_base >> 5) * 4096 + lane * 8;
+    const bf16_t* v0 = vb + (size_t)(key_base >> 5) * 4096 + lane * 8;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int key = key_base + 8 * (ln >> 2) + 4 * h + (ln & 3);
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            f.k[h][ks] = *reinterpret_cast<const uint4*>(kb + (size_t)key * 128 + ks * 32 + lg * 8);
-    }
+        for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = *reinterpret_cast<const uint4*>(k0 + (h * 4 + ks) * 512);
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-        f.v[dt] = *reinterpret_cast<const uint4*>(vb + (size_t)(dt * 16 + ln) * Smax + key_base + 8 * lg);
+    for (int dt = 0; dt < 8; ++dt) f.v[dt] = *reinterpret_cast<const uint4*>(v0 + dt * 512);
 }
 
 struct AttnState {
@@ -368,7 +387,9 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
                 const float o1 = __fadd_rn(__fmul_rn(bb, cs.x), __fmul_rn(a, cs.y));
                 const uint32_t pk = pack2(o0, o1);
                 if (pi < G * (HD / 2)) s_q[pi / (HD / 2)][(pi % (HD / 2))] = pk;
-                else s_kn[d / 2] = pk;
+                else {
+                    s_kn[d / 2] = pk;
+                }
             } else {
                 s_vn[d] = f2bf(a);
                 s_vn[d + 1] = f2bf(bb);
@@ -417,8 +438,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     }
     if (FUSED && split == nsplit - 1) {      // the split owning the newest key stores it (cache for later steps)
         const int t = threadIdx.x;
-        if (t < HD / 2) *reinterpret_cast<uint32_t*>(kb + (size_t)pos * HD + 2 * t) = s_kn[t];
-        else if (t < HD / 2 + HD) reinterpret_cast<uint16_t*>(vb)[(size_t)(t - HD / 2) * Smax + pos] = s_vn[t - HD / 2];
+        if (t < HD / 2) *reinterpret_cast<uint32_t*>(kb + k_off(pos, t >> 2) + ((2 * t) & 7)) = s_kn[t];
+        else if (t < HD / 2 + HD) reinterpret_cast<uint16_t*>(vb)[v_off(pos, t - HD / 2)] = s_vn[t - HD / 2];
     }
     // merge the 4 waves
     if (lg == 0) { s_m[w][ln] = st.m; s_l[w][ln] = st.l; }
@@ -509,11 +530,10 @@ __global__ __launch_bounds__(256) void k_attn_prefill(const bf16_t* q, const bf1
     // p = exp(s - max) summed in fp32 and rounded to bf16 for the P.V product.
     auto score = [&](int key) -> float {
         float acc = 0.f;
-        const uint4* kr = reinterpret_cast<const uint4*>(kb + (size_t)key * HD);
 #pragma unroll
         for (int i = 0; i < HD / 8; ++i) {
             float a[8], bq[8];
-            unpack8(kr[i], a);
+            unpack8(*reinterpret_cast<const uint4*>(kb + k_off(key, i)), a);
             unpack8(sq[w][i], bq);
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc += a[e] * bq[e];

@@ -12,7 +12,8 @@ Design (MI355X-first):
     completion are no-ops (every kernel checks the word).
   * Weights are bf16 in HBM in the engine's layouts: 9 embedding tables stacked
     [9][1026][D], the 9 heads stacked [9*1026][D], fc1 rows interleaved for the fused
-    SwiGLU epilogue. The KV cache is [R][Hkv][Smax][hd] (K) + [R][Hkv][hd][Smax] (V^T).
+    SwiGLU epilogue, GEMM weights fragment-packed (zk_pack_weights). The KV cache stores
+    per (row, kv head) 32-key slices in MFMA-fragment order (zonos_amd.kvlayout).
   * torch is plumbing only: it allocates device memory and provides the stream.
 """
 from __future__ import annotations
