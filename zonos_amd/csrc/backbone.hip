@@ -10,10 +10,7 @@
 //                  the 4 query heads of a KV head on the B side), k_attn_combine merges splits.
 //   k_attn_prefill: causal prefill attention, one wave per query, 64-key chunks.
 //
-// KV cache layout (engine-owned, not the reference's [R,S,2,Hkv,hd]):
-//   K   [R][Hkv][Smax][hd]   -- a key row is 256 contiguous bytes (A-operand loads)
-//   V^T [R][Hkv][hd][Smax]   -- 8 consecutive keys of one channel are contiguous
-//                               (B-operand loads of P.V)
+// KV cache layout: see "KV cache layout" below (32-key slices in MFMA-fragment order).
 #include "common.h"
 #include "../../include/zonos_hip.h"
 #include <algorithm>
@@ -79,6 +76,7 @@ ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, 
 }
 
 constexpr int LN_NT = 256;
+constexpr int RL_MAXS = 8;    // split-K slabs k_resid_ln reduces with all loads in flight
 constexpr int MAX_N8 = 4;     // D <= 8192
 
 template <int N8>
@@ -145,17 +143,35 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
         if (c >= D) continue;
         const float* p = part + (size_t)row * D + c;
         float acc[8];
-        {
+        if (nsplit <= RL_MAXS) {
+            // every slab load issued before the first add (clamped index, sum masked), so the
+            // row costs one memory round trip instead of nsplit; same left-to-right fp32 sum
+            float4 a0[RL_MAXS], a1[RL_MAXS];
+#pragma unroll
+            for (int s = 0; s < RL_MAXS; ++s) {
+                const float* ps = p + (size_t)min(s, nsplit - 1) * slab;
+                a0[s] = *reinterpret_cast<const float4*>(ps);
+                a1[s] = *reinterpret_cast<const float4*>(ps + 4);
+            }
+            acc[0] = a0[0].x; acc[1] = a0[0].y; acc[2] = a0[0].z; acc[3] = a0[0].w;
+            acc[4] = a1[0].x; acc[5] = a1[0].y; acc[6] = a1[0].z; acc[7] = a1[0].w;
+#pragma unroll
+            for (int s = 1; s < RL_MAXS; ++s)
+                if (s < nsplit) {
+                    acc[0] += a0[s].x; acc[1] += a0[s].y; acc[2] += a0[s].z; acc[3] += a0[s].w;
+                    acc[4] += a1[s].x; acc[5] += a1[s].y; acc[6] += a1[s].z; acc[7] += a1[s].w;
+                }
+        } else {
             const float4 a0 = *reinterpret_cast<const float4*>(p);
             const float4 a1 = *reinterpret_cast<const float4*>(p + 4);
             acc[0] = a0.x; acc[1] = a0.y; acc[2] = a0.z; acc[3] = a0.w;
             acc[4] = a1.x; acc[5] = a1.y; acc[6] = a1.z; acc[7] = a1.w;
-        }
-        for (int s = 1; s < nsplit; ++s) {
-            const float4 a0 = *reinterpret_cast<const float4*>(p + s * slab);
-            const float4 a1 = *reinterpret_cast<const float4*>(p + s * slab + 4);
-            acc[0] += a0.x; acc[1] += a0.y; acc[2] += a0.z; acc[3] += a0.w;
-            acc[4] += a1.x; acc[5] += a1.y; acc[6] += a1.z; acc[7] += a1.w;
+            for (int s = 1; s < nsplit; ++s) {
+                const float4 b0 = *reinterpret_cast<const float4*>(p + s * slab);
+                const float4 b1 = *reinterpret_cast<const float4*>(p + s * slab + 4);
+                acc[0] += b0.x; acc[1] += b0.y; acc[2] += b0.z; acc[3] += b0.w;
+                acc[4] += b1.x; acc[5] += b1.y; acc[6] += b1.z; acc[7] += b1.w;
+            }
         }
         float xi[8];
         unpack8(*reinterpret_cast<const uint4*>(x_in + (size_t)row * D + c), xi);
