@@ -243,6 +243,17 @@ int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* 
 int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias,
                    float* out, const int32_t* lens, int scale, void* stream);
 
+/* ------------------------------------------------------------------ codes_to_wavs post-processing
+ * Loudness of each decoded utterance as normalize_loudness measures it (autoencoder.py:172-186
+ * -> pyloudnorm 0.1.1 Meter(rate, block).integrated_loudness, BS.1770-4 K-weighting + gating;
+ * block 0.4 s if the utterance is longer than 2 s else 0.1 s). wav fp32 [B][T] (row b valid for
+ * lens[b] samples, NULL = T). gains[b] = 10^((target - L_b)/20), loudness[b] = L_b; utterances
+ * shorter than one block get gain 1 and loudness NaN (the reference's except path).
+ * scratch: fp64, B*T + B*zk_loudness_max_blocks(T, rate) elements. */
+int zk_loudness_max_blocks(long T, int rate);
+int zk_loudness_gains(const float* wav, int B, long T, const int32_t* lens, int rate, double target_lufs,
+                      double* scratch, double* gains, double* loudness, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,7 @@ _SIGS = {
     "zk_dac_rvq_decode_cl": [P, I, I, I, L, P, I, I, I, P, P, P],
     "zk_dac_conv_cl": [P, I, I, I, P, L, P, I, I, I, I, I, I, I, I, I, P, P, P, P, I, P, I, I, P],
     "zk_dac_tail_cl": [P, I, I, I, P, P, P, P, I, P],
+    "zk_loudness_gains": [P, I, L, P, I, C.c_double, P, P, P, P],
 }
 
 _lib = None
@@ -96,12 +97,14 @@ def load():
         fn.restype = C.c_int
     lib.zk_last_error.restype = C.c_char_p
     lib.zk_last_error.argtypes = []
+    lib.zk_loudness_max_blocks.restype = C.c_int
+    lib.zk_loudness_max_blocks.argtypes = [L, I]
     _lib = lib
     return lib
 
 
 def exported_symbols() -> list[str]:
-    return list(_SIGS) + ["zk_last_error"]
+    return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks"]
 
 
 def call(name: str, *args):

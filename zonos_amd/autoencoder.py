@@ -362,9 +362,12 @@ class DACAutoencoder:
     def decode_list(self, codes) -> list:
         return self.decoder.decode_list(codes)
 
-    # ---- post-processing of codes_to_wavs (autoencoder.py:49-90, 172-245) -- host side, per file
+    # ---- post-processing of codes_to_wavs (autoencoder.py:49-90, 172-245)
     @staticmethod
     def trim_silence(wav: torch.Tensor, threshold: float = 1e-5, frame_size: int = 512) -> torch.Tensor:
+        """autoencoder.py:49-90 as written: the tail loop's first frame is wav[:, -512:-0] (empty,
+        its mean is nan and never above the threshold), a found tail frame cuts at -(i+1)*512."""
+        assert wav.ndim == 2 and wav.shape[0] == 1, "Expected mono audio tensor"
         n = min((wav.shape[1] // frame_size) // 4, 16)
         start, end = 0, wav.shape[1]
         for i in range(n):
@@ -372,58 +375,93 @@ class DACAutoencoder:
                 start = i * frame_size
                 break
         for i in range(n):
-            fr = wav[:, -((i + 1) * frame_size): -i * frame_size] if i else wav[:, -frame_size:]
-            if fr.pow(2).mean() > threshold:
-                end = wav.shape[1] - (i + 1) * frame_size
+            if wav[:, -((i + 1) * frame_size): -i * frame_size].pow(2).mean() > threshold:
+                end = -((i + 1) * frame_size)
                 break
         return wav[:, start:end] if (start > 0 or end < wav.shape[1]) else wav
 
+    def loudness_gains(self, wavs: list, target_lufs: float = -23.0) -> list:
+        """Per-utterance gains of normalize_loudness (pyloudnorm BS.1770 integrated loudness),
+        measured for the whole list in one batched GPU pass (zk_loudness_gains)."""
+        wavs = [w for w in wavs]
+        if not wavs:
+            return []
+        dev = self.decoder.device
+        T = max(int(w.shape[-1]) for w in wavs)
+        T = (T + 3) // 4 * 4
+        B = len(wavs)
+        batch = torch.zeros(B, T, device=dev)
+        for i, w in enumerate(wavs):
+            batch[i, :w.shape[-1]] = w.reshape(-1).to(dev, torch.float32)
+        lens = torch.tensor([int(w.shape[-1]) for w in wavs], dtype=torch.int32, device=dev)
+        nb = _lib.load().zk_loudness_max_blocks(T, int(self.sampling_rate))
+        scratch = torch.empty(B * T + B * max(nb, 1), dtype=torch.float64, device=dev)
+        gains = torch.empty(B, dtype=torch.float64, device=dev)
+        loud = torch.empty(B, dtype=torch.float64, device=dev)
+        call("zk_loudness_gains", ptr(batch), B, T, ptr(lens), int(self.sampling_rate), float(target_lufs),
+             ptr(scratch), ptr(gains), ptr(loud), _lib.stream_ptr(dev))
+        return gains.cpu().tolist()
+
     def normalize_loudness(self, audio, sr, target_lufs=-19.0):
-        try:
-            import pyloudnorm
-            block = 0.400 if audio.shape[1] > 2.0 * sr else 0.100
-            loud = pyloudnorm.Meter(sr, block_size=block).integrated_loudness(audio.cpu().numpy().T)
-            return audio * (10 ** ((target_lufs - loud) / 20.0))
-        except Exception:
-            return audio
+        """autoencoder.py:172-186: audio * 10^((target - loudness)/20); unchanged if too short."""
+        assert sr == self.sampling_rate
+        return audio * self.loudness_gains([audio], target_lufs)[0]
 
     def codes_to_wavs(self, codes) -> list:
-        if isinstance(codes, torch.Tensor):
-            if codes.dim() == 2:
-                codes = [codes]
-            elif codes.dim() == 3:
-                codes = [codes[i] for i in range(codes.shape[0])]
-            else:
-                raise ValueError(f"Invalid shape for codes: {codes.shape}")
-        wavs = self.decode_list(codes)
+        """autoencoder.py:188-245: decode (one batched, length-masked GPU pass instead of one
+        decode per utterance), loudness to -23 LUFS (batched GPU measurement), silence trim,
+        512-sample linear fade-in, log fade-out over up to 20 blocks. Returns CPU [1, n] fp32."""
+        if isinstance(codes, list):
+            code_list = [c if c.dim() == 3 else c.unsqueeze(0) for c in codes]
+            items = [c[i] for c in code_list for i in range(c.shape[0])]
+        elif codes.dim() == 2:
+            items = [codes]
+        elif codes.dim() == 3:
+            items = [codes[i] for i in range(codes.shape[0])]
+        else:
+            raise ValueError(f"Invalid shape for codes: {codes.shape}. Expected [num_codebooks, num_codes] or "
+                             f"[batch_size, num_codebooks, num_codes]")
+        wavs = self.decode_list(items)                     # empty utterances skipped (autoencoder.py:221-223)
+        gains = self.loudness_gains(wavs, -23.0)
         out = []
-        for wav in wavs:
-            wav = wav.cpu()
-            wav = self.normalize_loudness(wav, self.sampling_rate, -23.0)
+        for wav, g in zip(wavs, gains):
+            wav = wav.cpu() * g
             wav = self.trim_silence(wav)
-            bs = 512
-            wav[:, :bs] *= torch.linspace(0, 1, min(bs, wav.shape[1])).unsqueeze(0)[:, :wav[:, :bs].shape[1]]
-            nb = min((wav.shape[1] // bs) // 4, 20)
+            blocksize = 512
+            wav[:, :blocksize] *= torch.linspace(0, 1, blocksize, device=wav.device).unsqueeze(0)
+            nb = min((wav.shape[1] // blocksize) // 4, 20)
             if nb > 0:
-                wav[:, -(nb * bs):] *= torch.logspace(0, -10, nb * bs).unsqueeze(0)
+                wav[:, -(nb * blocksize):] *= torch.logspace(0, -10, nb * blocksize, device=wav.device).unsqueeze(0)
             out.append(wav)
         return out
 
     def save_codes(self, paths, codes) -> None:
+        """autoencoder.py:247-268: codes_to_wavs + one file per waveform. torchaudio.save of a
+        float32 tensor writes a 32-bit IEEE-float WAV; the same format is written here
+        (torchaudio is not a dependency of this package)."""
         if isinstance(paths, str):
             paths = [paths]
         wavs = self.codes_to_wavs(codes)
         assert len(paths) == len(wavs), f"Number of paths ({len(paths)}) must match number of codes ({len(wavs)})"
-        import wave
-
-        import numpy as np
         for p, w in zip(paths, wavs):
-            pcm = (w.clamp(-1, 1).squeeze(0).numpy() * 32767.0).astype(np.int16)
-            with wave.open(p, "wb") as f:
-                f.setnchannels(1)
-                f.setsampwidth(2)
-                f.setframerate(self.sampling_rate)
-                f.writeframes(pcm.tobytes())
+            write_wav_f32(p, w, self.sampling_rate)
+
+
+def write_wav_f32(path: str, wav: torch.Tensor, sr: int) -> None:
+    """RIFF/WAVE, WAVE_FORMAT_IEEE_FLOAT (3), 32 bit, channels = wav.shape[0] (interleaved)."""
+    import struct
+
+    x = wav.detach().to("cpu", torch.float32)
+    x = x.unsqueeze(0) if x.dim() == 1 else x
+    ch, n = x.shape
+    data = x.t().contiguous().numpy().tobytes()
+    fmt = struct.pack("<HHIIHH", 3, ch, sr, sr * ch * 4, ch * 4, 32)
+    fact = struct.pack("<I", n)
+    with open(path, "wb") as f:
+        f.write(b"RIFF" + struct.pack("<I", 4 + (8 + len(fmt)) + (8 + len(fact)) + (8 + len(data))) + b"WAVE")
+        f.write(b"fmt " + struct.pack("<I", len(fmt)) + fmt)
+        f.write(b"fact" + struct.pack("<I", len(fact)) + fact)
+        f.write(b"data" + struct.pack("<I", len(data)) + data)
 
 
 def _load_safetensors_dir(path: str):
