@@ -78,9 +78,12 @@ int zk_layernorm(const void* x, const void* w, const void* b, float eps, int row
                  void* y, void* stream);
 
 /* x_out = bf16(x_in + bf16(sum_s part[s])) ; xn = LayerNorm(x_out) (_torch.py:100-101).
+ * ln_on_sum = 1: xn = LayerNorm(x_in + bf16(sum)) of the fp32 sum before rounding (mamba_ssm
+ * layer_norm_fn with prenorm, the hybrid backbone's fused add + norm).
  * part: fp32 [nsplit][rows][D] split-K slabs of the preceding projection. */
 int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, const void* b,
-                float eps, int rows, int D, void* x_out, void* xn_out, const int32_t* skip, void* stream);
+                float eps, int rows, int D, void* x_out, void* xn_out, int ln_on_sum,
+                const int32_t* skip, void* stream);
 
 /* C = A[M][K] . W[N][K]^T (nn.Linear, bias-free). bf16 in, fp32 accumulation (MFMA).
  * mode 0: fp32 split-K slabs Cpart[split][M][N] (nsplit = K-split count);
@@ -106,11 +109,14 @@ int zk_pack_weights(const void* w, int N, int K, void* out, void* stream);
  * 8 KB stored in MFMA-fragment order (backbone.hip k_off / v_off; zonos_amd.kvlayout):
  *   K: [R][Hkv][Smax/32][h 2][ks 4][lane 64][8],  V: [R][Hkv][Smax/32][dt 8][lane 64][8].
  * v_rows (nullable): also write V as [R][Hkv][S][hd] (prefill scratch).
+ * rope_neox = 0: interleaved pairs (2j, 2j+1) (the transformer); 1: GPT-NeoX pairs (j, j+hd/2)
+ * (mamba_ssm MHA via flash_attn RotaryEmbedding, interleaved=False; hybrid backbone). freqs is
+ * then the bf16-rounded cos/sin cache (oracle/hybrid_ref.py rotary_table).
  * rows = R*S tokens ordered r*S + t. */
 int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv, int hd,
                 const float* freqs, int pos0, const int32_t* pos_dev,
                 void* q_out, void* k_cache, void* vt_cache, int Smax, void* v_rows,
-                const int32_t* skip, void* stream);
+                int rope_neox, const int32_t* skip, void* stream);
 
 /* Scaled-dot-product attention over the cache (F.scaled_dot_product_attention,
  * _torch.py:136; GQA, scale 1/sqrt(hd)).
@@ -129,7 +135,7 @@ int zk_attn_prefill(const void* q, const void* k_cache, const void* v_rows, int 
  * RoPE, writes the new K / V^T cache entries and attends over keys [0, ctx). q is not stored. */
 int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
                        void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
-                       const int32_t* ctx_dev, float* work, int nsplit, void* out,
+                       const int32_t* ctx_dev, float* work, int nsplit, void* out, int rope_neox,
                        const int32_t* skip, void* stream);
 
 /* ------------------------------------------------------------------ graphs and timing
@@ -242,6 +248,29 @@ int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* 
  * (s = fp32 output of the final Snake, zk_dac_conv_cl with s_f32 = 1; modeling_dac.py:437-439). */
 int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias,
                    float* out, const int32_t* lens, int scale, void* stream);
+
+/* ------------------------------------------------------------------ hybrid backbone: Mamba2 mixer
+ * (zonos/backbone/_mamba_ssm.py -> mamba_ssm Mamba2; restated in oracle/hybrid_ref.py).
+ * in_proj output columns [z (d_inner) | xBC (conv_dim = d_inner + 2 d_state) | dt (nheads)].
+ * Conv state bf16 [R][conv_dim][4] (last 4 inputs), double-buffered by step parity: the step at
+ * position *pos_dev reads buffer (pos & 1) of {a, b} and writes the other. SSM state bf16
+ * [R][nheads][headdim][d_state]. A = -exp(A_log), dt_bias, D fp32 [nheads]; conv_w fp32
+ * [conv_dim][4], conv_b fp32 [conv_dim]. yz (fp32 [rows][d_inner]) = bf16(C.h + D x) * silu(z),
+ * normalised by zk_gated_rmsnorm (RMSNormGated, norm_before_gate=False) into the out_proj input.
+ * (headdim, d_state) in {(64,128), (64,64), (32,64)}. */
+int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
+                  int d_state, const float* conv_w, const float* conv_b, void* conv_state_a,
+                  void* conv_state_b, const int32_t* pos_dev, void* ssm_state, const float* A,
+                  const float* dt_bias, const float* D, float* yz, const int32_t* skip, void* stream);
+/* prefill over S positions per row: zx = in_proj output fp32 [R*S][cols] (split 1); xc_scratch
+ * bf16 [R*S][conv_dim]; conv_state receives the last 4 inputs (the buffer the first decode step
+ * reads); ssm_state receives the final state (bf16). */
+int zk_mamba_prefill(const float* zx, int R, int S, int d_inner, int nheads, int headdim, int d_state,
+                     const float* conv_w, const float* conv_b, void* xc_scratch, void* conv_state,
+                     void* ssm_state, const float* A, const float* dt_bias, const float* D, float* yz,
+                     void* stream);
+int zk_gated_rmsnorm(const float* g, int rows, int d_inner, const float* w, float eps, void* out,
+                     const int32_t* skip, void* stream);
 
 /* ------------------------------------------------------------------ codes_to_wavs post-processing
  * Loudness of each decoded utterance as normalize_loudness measures it (autoencoder.py:172-186

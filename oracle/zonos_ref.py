@@ -191,7 +191,11 @@ def attention(W, cfg, i, x, kv: KVCache, fc):
 
 def backbone(W, cfg: BackboneCfg, h: torch.Tensor, kv: KVCache, freqs: torch.Tensor) -> torch.Tensor:
     """TorchZonosBackbone.forward (_torch.py:73-80) with TransformerBlock (_torch.py:99-102)
-    and FeedForward (_torch.py:150-152). Pre-LN LayerNorm *with bias*, SwiGLU (y, gate)."""
+    and FeedForward (_torch.py:150-152). Pre-LN LayerNorm *with bias*, SwiGLU (y, gate).
+    A HybridCfg routes to the hybrid backbone restatement (oracle/hybrid_ref.py)."""
+    from . import hybrid_ref
+    if isinstance(cfg, hybrid_ref.HybridCfg):
+        return hybrid_ref.backbone(W, cfg, h, kv, freqs)
     R, S, D = h.shape
     pos = torch.arange(S)[None, :] + kv.lengths[:, None]
     fc = freqs[pos]
@@ -328,8 +332,13 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
     P = 0 if audio_prefix_codes is None else audio_prefix_codes.shape[2]
     T = P + max_new_tokens
     Lc = prefix_conditioning.shape[1]
-    kv = KVCache(cfg, 2 * B, Lc + T + 9)
-    freqs = rope_table(16384, cfg.head_dim)
+    from . import hybrid_ref
+    if isinstance(cfg, hybrid_ref.HybridCfg):          # MambaSSMZonosBackbone (model.py:204-208 cache)
+        kv = hybrid_ref.HybridCache(cfg, 2 * B, Lc + T + 9)
+        freqs = hybrid_ref.rotary_table(Lc + T + 16, cfg.head_dim, cfg.rotary_base)
+    else:
+        kv = KVCache(cfg, 2 * B, Lc + T + 9)
+        freqs = rope_table(16384, cfg.head_dim)
     codes = torch.full((B, 9, T), UNKNOWN)
     if audio_prefix_codes is not None:
         codes[..., :P] = audio_prefix_codes

@@ -149,9 +149,16 @@ def test_layernorm_and_resid_ln():
         xo = torch.empty_like(xd)
         xn = torch.empty_like(xd)
         pd = part.to(DEV)
-        call("zk_resid_ln", ptr(pd), 3, ptr(xd), ptr(wd), ptr(bd), 1e-5, rows, D, ptr(xo), ptr(xn), None, s)
+        call("zk_resid_ln", ptr(pd), 3, ptr(xd), ptr(wd), ptr(bd), 1e-5, rows, D, ptr(xo), ptr(xn), 0, None, s)
         assert (xo.float().cpu() - ref_x.float()).abs().max() < 0.07
         assert (xn.float().cpu() - ref_xn.float()).abs().max() < 0.06
+        # ln_on_sum (mamba_ssm layer_norm_fn prenorm): LN of the fp32 sum, residual stored bf16
+        xo2, xn2 = torch.empty_like(xd), torch.empty_like(xd)
+        call("zk_resid_ln", ptr(pd), 3, ptr(xd), ptr(wd), ptr(bd), 1e-5, rows, D, ptr(xo2), ptr(xn2), 1, None, s)
+        ssum = x.float() + part.sum(0).to(torch.bfloat16).float()
+        ref_xn2 = F.layer_norm(ssum, (D,), w.float(), b.float(), 1e-5)
+        assert torch.equal(xo2.cpu(), xo.cpu())
+        assert (xn2.float().cpu() - ref_xn2).abs().max() < 0.06
 
 
 def _attn_setup(R, S_ctx, H, Hk, hd, smax, seed=0):
@@ -187,9 +194,11 @@ def test_attention_decode(R, ctx, H, Hk, nsplit):
     assert (out.float().cpu() - ref).abs().max() < 2e-2
 
 
-@pytest.mark.parametrize("R,ctx,H,Hk,nsplit,gs", [(4, 1, 16, 4, 1, 4), (6, 37, 2, 1, 2, 2), (128, 300, 16, 4, 1, 4),
-                                                   (3, 700, 16, 4, 4, 8), (2, 129, 2, 1, 1, 1), (5, 256, 16, 4, 2, 3)])
-def test_attention_decode_fused_qkv_equals_separate(R, ctx, H, Hk, nsplit, gs):
+@pytest.mark.parametrize("R,ctx,H,Hk,nsplit,gs,neox", [(4, 1, 16, 4, 1, 4, 0), (6, 37, 2, 1, 2, 2, 0),
+                                                        (128, 300, 16, 4, 1, 4, 0), (3, 700, 16, 4, 4, 8, 0),
+                                                        (2, 129, 2, 1, 1, 1, 0), (5, 256, 16, 4, 2, 3, 0),
+                                                        (6, 300, 16, 4, 2, 4, 1), (128, 77, 16, 4, 1, 4, 1)])
+def test_attention_decode_fused_qkv_equals_separate(R, ctx, H, Hk, nsplit, gs, neox):
     """zk_attn_decode_qkv == zk_qkv_rope (at pos = ctx-1) + zk_attn_decode: bit-identical
     output and identical cache contents afterwards."""
     from zonos_amd._lib import call, ptr, stream_ptr
@@ -210,14 +219,14 @@ def test_attention_decode_fused_qkv_equals_separate(R, ctx, H, Hk, nsplit, gs):
     q = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
     out1 = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
     call("zk_qkv_rope", ptr(part), gs, R, 1, H, Hk, hd, ptr(freqs), ctx - 1, None, ptr(q), ptr(kc1), ptr(vt1), smax,
-         None, None, s)
+         None, neox, None, s)
     call("zk_attn_decode", ptr(q), ptr(kc1), ptr(vt1), R, H, Hk, hd, smax, ctx, None, ptr(work), nsplit, ptr(out1),
          None, s)
     # fused
     kc2, vt2 = kc0.clone(), vt0.clone()
     out2 = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
     call("zk_attn_decode_qkv", ptr(part), gs, ptr(freqs), ptr(kc2), ptr(vt2), R, H, Hk, hd, smax, ctx, None,
-         ptr(work), nsplit, ptr(out2), None, s)
+         ptr(work), nsplit, ptr(out2), neox, None, s)
     torch.cuda.synchronize()
     assert torch.equal(kc1, kc2) and torch.equal(vt1, vt2)
     assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max()
@@ -260,7 +269,7 @@ def test_qkv_rope_matches_oracle():
     vrows = torch.zeros(R, Hk, S, hd, dtype=torch.bfloat16, device=DEV)
     pd, fd = part.to(DEV), fr.to(DEV)
     call("zk_qkv_rope", ptr(pd), 2, R, S, H, Hk, hd, ptr(fd), pos0, None, ptr(q), ptr(kc), ptr(vt), smax, ptr(vrows),
-         None, stream_ptr())
+         0, None, stream_ptr())
     # slab sums in a different order can flip one bf16 rounding; then RoPE is exact fp32
     assert (q.float().cpu() - q_ref.float()).abs().max() < 0.05
     from zonos_amd.kvlayout import unpack_k, unpack_v

@@ -44,13 +44,16 @@ _SIGS = {
     "zk_delay_revert": [P, I, I, I, P, P],
     "zk_embed_codes": [P, I, I, I, L, L, P, I, P, I, I, I, P, I, I, P, P, F, P, P, P],
     "zk_layernorm": [P, P, P, F, I, I, P, P],
-    "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, P, P],
+    "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, I, P, P],
     "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
     "zk_permute_fc1": [P, I, I, P, P],
     "zk_pack_weights": [P, I, I, P, P],
-    "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, P, P],
+    "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, I, P, P],
     "zk_attn_decode": [P, P, P, I, I, I, I, I, I, P, P, I, P, P, P],
-    "zk_attn_decode_qkv": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, P, P, P],
+    "zk_attn_decode_qkv": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, P, I, P, P],
+    "zk_mamba_step": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P],
+    "zk_mamba_prefill": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
+    "zk_gated_rmsnorm": [P, I, I, P, F, P, P, P],
     "zk_attn_prefill": [P, P, P, I, I, I, I, I, I, P, P],
     "zk_sample_heads": [P, I, C.POINTER(GenState), C.POINTER(SamplingParams), I, I, P, P],
     "zk_eos_step": [C.POINTER(GenState), I, I, P],

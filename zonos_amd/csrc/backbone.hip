@@ -130,7 +130,8 @@ __global__ __launch_bounds__(LN_NT) void k_layernorm(const bf16_t* x, const bf16
 template <int N8>
 __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nsplit, const bf16_t* x_in,
                                                     const bf16_t* w, const bf16_t* b, float eps, int rows, int D,
-                                                    bf16_t* x_out, bf16_t* xn_out, const int32_t* skip) {
+                                                    bf16_t* x_out, bf16_t* xn_out, int ln_on_sum,
+                                                    const int32_t* skip) {
     __shared__ float red[LN_NT / 64];
     if (skip && *skip) return;
     const int row = blockIdx.x;
@@ -175,14 +176,30 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
         }
         float xi[8];
         unpack8(*reinterpret_cast<const uint4*>(x_in + (size_t)row * D + c), xi);
+        // transformer (_torch.py:100-101): x = bf16(x + bf16(proj)), LN of the rounded x;
+        // ln_on_sum (mamba_ssm layer_norm_fn prenorm): LN of the fp32 sum, residual stored bf16
 #pragma unroll
-        for (int e = 0; e < 8; ++e) xv[j * 8 + e] = round_bf(xi[e] + round_bf(acc[e]));
+        for (int e = 0; e < 8; ++e) xv[j * 8 + e] = xi[e] + round_bf(acc[e]);
         *reinterpret_cast<uint4*>(x_out + (size_t)row * D + c) = pack8(xv + 8 * j);
+        if (!ln_on_sum) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[j * 8 + e] = round_bf(xv[j * 8 + e]);
+        }
     }
     ln_row<LN_NT, N8>(xv, w, b, eps, D, xn_out + (size_t)row * D, red);
 }
 
 // ------------------------------------------------------------------ in_proj epilogue
+// RoPE pair j (0..hd/2-1) of a head: interleaved (_torch.py:18-30: dims 2j, 2j+1) or, NEOX,
+// GPT-NeoX "rotate half" (flash_attn apply_rotary, interleaved=False: dims j, j + hd/2).
+// Both use (cos, sin) entry j of the position's [hd/2][2] table.
+template <bool NEOX>
+ZK_DEV void rope_dims(int j, int hd, int& d0, int& d1) {
+    d0 = NEOX ? j : 2 * j;
+    d1 = NEOX ? j + hd / 2 : 2 * j + 1;
+}
+
+template <bool NEOX>
 __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv,
                                                   int hd, const float* freqs, int pos0, const int32_t* pos_dev,
                                                   bf16_t* q_out, bf16_t* kc, bf16_t* vt, int Smax, bf16_t* v_rows,
@@ -196,31 +213,37 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit,
     const float* p = part + (size_t)row * N;
     const float* fc = freqs + (size_t)pos * hd;     // [hd/2][2]
     for (int pi = threadIdx.x; pi < N / 2; pi += blockDim.x) {
-        const int col = 2 * pi;
-        float a = p[col], bb = p[col + 1];
-        for (int s = 1; s < nsplit; ++s) { a += p[s * slab + col]; bb += p[s * slab + col + 1]; }
+        const int head = pi / (hd / 2), j = pi % (hd / 2);     // head over q | k | v heads
+        int d0, d1;
+        rope_dims<NEOX>(j, hd, d0, d1);
+        const int c0 = head * hd + d0, c1 = head * hd + d1;
+        float a = p[c0], bb = p[c1];
+        for (int s = 1; s < nsplit; ++s) { a += p[s * slab + c0]; bb += p[s * slab + c1]; }
         a = round_bf(a); bb = round_bf(bb);
-        const int d = col % hd;
-        if (col < (H + Hkv) * hd) {
-            const float c = fc[d], sn = fc[d + 1];   // pair index d/2 -> (cos, sin) at [d/2][0..1]
+        if (head < H + Hkv) {
+            const float c = fc[2 * j], sn = fc[2 * j + 1];
             const float o0 = __fsub_rn(__fmul_rn(a, c), __fmul_rn(bb, sn));
             const float o1 = __fadd_rn(__fmul_rn(bb, c), __fmul_rn(a, sn));
-            const uint32_t pk = pack2(o0, o1);
-            if (col < H * hd) {
-                *reinterpret_cast<uint32_t*>(q_out + (size_t)row * H * hd + col) = pk;
+            const bf16_t b0 = f2bf(o0), b1 = f2bf(o1);
+            if (head < H) {
+                bf16_t* qr = q_out + (size_t)row * H * hd + head * hd;
+                qr[d0] = b0;
+                qr[d1] = b1;
             } else {
-                const int g = (col - H * hd) / hd;
-                *reinterpret_cast<uint32_t*>(kc + ((size_t)r * Hkv + g) * Smax * hd + k_off(pos, d >> 3) + (d & 7)) = pk;
+                bf16_t* kb = kc + ((size_t)r * Hkv + (head - H)) * Smax * hd;
+                kb[k_off(pos, d0 >> 3) + (d0 & 7)] = b0;
+                kb[k_off(pos, d1 >> 3) + (d1 & 7)] = b1;
             }
         } else {
-            const int g = (col - (H + Hkv) * hd) / hd;
+            const int g = head - H - Hkv;
             bf16_t* base = vt + ((size_t)r * Hkv + g) * Smax * hd;
             const bf16_t va = f2bf(a), vb = f2bf(bb);
-            base[v_off(pos, d)] = va;
-            base[v_off(pos, d + 1)] = vb;
+            base[v_off(pos, d0)] = va;
+            base[v_off(pos, d1)] = vb;
             if (v_rows) {
-                *reinterpret_cast<uint32_t*>(v_rows + (((size_t)r * Hkv + g) * S + t) * hd + d) =
-                    (uint32_t)va | ((uint32_t)vb << 16);
+                bf16_t* vr = v_rows + (((size_t)r * Hkv + g) * S + t) * hd;
+                vr[d0] = va;
+                vr[d1] = vb;
             }
         }
     }
@@ -339,7 +362,7 @@ ZK_DEV void patch_kv(KVFrag& f, const uint32_t* s_kn, const uint16_t* s_vn, int 
 // reduces the split-K slabs of its own 4 query heads + 1 KV head (768 columns), applies RoPE,
 // keeps q in LDS and (the split that owns the newest key) stores the new K / V^T entries
 // before the key loop reads them. One launch per layer instead of two.
-template <bool FUSED>
+template <bool FUSED, bool NEOX = false>
 __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H,
                                                         int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
                                                         float* work, float scale, bf16_t* out, const int32_t* skip,
@@ -379,36 +402,38 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
         const size_t slab = (size_t)R * N;
         const float* prow = part + (size_t)r * N;
         const float* fc = freqs + (size_t)pos * HD;
+        uint16_t* q16 = reinterpret_cast<uint16_t*>(&s_q[0][0]);
+        uint16_t* k16 = reinterpret_cast<uint16_t*>(s_kn);
         for (int pi = threadIdx.x; pi < (G + 2) * (HD / 2); pi += 256) {
-            int col;
-            if (pi < G * (HD / 2)) col = g * G * HD + 2 * pi;
-            else if (pi < (G + 1) * (HD / 2)) col = H * HD + g * HD + 2 * (pi - G * (HD / 2));
-            else col = (H + Hkv) * HD + g * HD + 2 * (pi - (G + 1) * (HD / 2));
+            const int hp = pi / (HD / 2), j = pi % (HD / 2);      // hp < G: q head g*G+hp; G: k; G+1: v
+            int d0, d1;
+            rope_dims<NEOX>(j, HD, d0, d1);
+            const int cb = hp < G ? (g * G + hp) * HD : (hp == G ? H * HD + g * HD : (H + Hkv) * HD + g * HD);
             // all slab loads issued together (clamped slab index, select after) -- same
             // left-to-right fp32 sum as k_qkv_rope
-            float2 v[AT_MAXGS];
+            float v0[AT_MAXGS], v1[AT_MAXGS];
 #pragma unroll
-            for (int sl = 0; sl < AT_MAXGS; ++sl)
-                v[sl] = *reinterpret_cast<const float2*>(prow + (size_t)min(sl, gsplit - 1) * slab + col);
-            const int d = col % HD;
-            const float2 cs = *reinterpret_cast<const float2*>(fc + d);
-            float a = v[0].x, bb = v[0].y;
+            for (int sl = 0; sl < AT_MAXGS; ++sl) {
+                const float* ps = prow + (size_t)min(sl, gsplit - 1) * slab + cb;
+                v0[sl] = ps[d0];
+                v1[sl] = ps[d1];
+            }
+            const float2 cs = *reinterpret_cast<const float2*>(fc + 2 * j);
+            float a = v0[0], bb = v1[0];
 #pragma unroll
             for (int sl = 1; sl < AT_MAXGS; ++sl)
-                if (sl < gsplit) { a += v[sl].x; bb += v[sl].y; }
+                if (sl < gsplit) { a += v0[sl]; bb += v1[sl]; }
             a = round_bf(a);
             bb = round_bf(bb);
-            if (pi < (G + 1) * (HD / 2)) {
+            if (hp <= G) {
                 const float o0 = __fsub_rn(__fmul_rn(a, cs.x), __fmul_rn(bb, cs.y));
                 const float o1 = __fadd_rn(__fmul_rn(bb, cs.x), __fmul_rn(a, cs.y));
-                const uint32_t pk = pack2(o0, o1);
-                if (pi < G * (HD / 2)) s_q[pi / (HD / 2)][(pi % (HD / 2))] = pk;
-                else {
-                    s_kn[d / 2] = pk;
-                }
+                uint16_t* dst = hp < G ? q16 + hp * HD : k16;
+                dst[d0] = f2bf(o0);
+                dst[d1] = f2bf(o1);
             } else {
-                s_vn[d] = f2bf(a);
-                s_vn[d + 1] = f2bf(bb);
+                s_vn[d0] = f2bf(a);
+                s_vn[d1] = f2bf(bb);
             }
         }
         __syncthreads();      // q, new k, new v in LDS
@@ -621,25 +646,31 @@ extern "C" int zk_layernorm(const void* x, const void* w, const void* b, float e
 }
 
 extern "C" int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, const void* b, float eps,
-                           int rows, int D, void* x_out, void* xn_out, const int32_t* skip, void* stream) {
+                           int rows, int D, void* x_out, void* xn_out, int ln_on_sum, const int32_t* skip,
+                           void* stream) {
     ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_resid_ln: unsupported D=%d", D);
     ZK_REQUIRE(nsplit >= 1, "zk_resid_ln: nsplit must be >= 1");
     if (rows == 0) return 0;
     ZK_LN_DISPATCH(D, k_resid_ln, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, part, nsplit,
                        (const bf16_t*)x_in, (const bf16_t*)w, (const bf16_t*)b, eps, rows, D, (bf16_t*)x_out,
-                       (bf16_t*)xn_out, skip);
+                       (bf16_t*)xn_out, ln_on_sum, skip);
     ZK_CHECK_LAUNCH("zk_resid_ln");
     return 0;
 }
 
 extern "C" int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv, int hd, const float* freqs,
                            int pos0, const int32_t* pos_dev, void* q_out, void* k_cache, void* vt_cache, int Smax,
-                           void* v_rows, const int32_t* skip, void* stream) {
+                           void* v_rows, int rope_neox, const int32_t* skip, void* stream) {
     ZK_REQUIRE(hd % 2 == 0 && nsplit >= 1, "zk_qkv_rope: bad args");
     if (R * S == 0) return 0;
-    hipLaunchKernelGGL(k_qkv_rope, dim3(R * S), dim3(256), 0, (hipStream_t)stream, part, nsplit, R, S, H, Hkv, hd,
-                       freqs, pos0, pos_dev, (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)vt_cache, Smax,
-                       (bf16_t*)v_rows, skip);
+    if (rope_neox)
+        hipLaunchKernelGGL(k_qkv_rope<true>, dim3(R * S), dim3(256), 0, (hipStream_t)stream, part, nsplit, R, S, H,
+                           Hkv, hd, freqs, pos0, pos_dev, (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)vt_cache, Smax,
+                           (bf16_t*)v_rows, skip);
+    else
+        hipLaunchKernelGGL(k_qkv_rope<false>, dim3(R * S), dim3(256), 0, (hipStream_t)stream, part, nsplit, R, S, H,
+                           Hkv, hd, freqs, pos0, pos_dev, (bf16_t*)q_out, (bf16_t*)k_cache, (bf16_t*)vt_cache, Smax,
+                           (bf16_t*)v_rows, skip);
     ZK_CHECK_LAUNCH("zk_qkv_rope");
     return 0;
 }
@@ -668,8 +699,8 @@ extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt
 
 extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
                                   void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
-                                  const int32_t* ctx_dev, float* work, int nsplit, void* out, const int32_t* skip,
-                                  void* stream) {
+                                  const int32_t* ctx_dev, float* work, int nsplit, void* out, int rope_neox,
+                                  const int32_t* skip, void* stream) {
     ZK_REQUIRE(hd == 128, "zk_attn_decode_qkv: head_dim %d unsupported (128 only)", hd);
     ZK_REQUIRE(H % Hkv == 0 && H / Hkv <= AT_G, "zk_attn_decode_qkv: GQA group %d > %d", H / Hkv, AT_G);
     ZK_REQUIRE(Smax % AT_KB == 0, "zk_attn_decode_qkv: Smax=%d must be a multiple of %d", Smax, AT_KB);
@@ -684,9 +715,14 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
 #else
     const bf16_t* dbgq = nullptr;
 #endif
-    hipLaunchKernelGGL(k_attn_decode<true>, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq,
-                       (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out,
-                       skip, part, gemm_nsplit, freqs);
+    if (rope_neox)
+        hipLaunchKernelGGL((k_attn_decode<true, true>), dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq,
+                           (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale,
+                           (bf16_t*)out, skip, part, gemm_nsplit, freqs);
+    else
+        hipLaunchKernelGGL((k_attn_decode<true, false>), dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream,
+                           dbgq, (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale,
+                           (bf16_t*)out, skip, part, gemm_nsplit, freqs);
     ZK_CHECK_LAUNCH("zk_attn_decode_qkv");
     if (nsplit > 1) {
         hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, nsplit,

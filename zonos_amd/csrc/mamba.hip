@@ -1,0 +1,279 @@
+// Mamba2 mixer of the hybrid backbone (zonos/backbone/_mamba_ssm.py -> mamba_ssm Mamba2,
+// restated in oracle/hybrid_ref.py) for gfx950.
+//
+//   k_mamba_step   : decode. One workgroup per (head, row): split-K slab reduction of the
+//                    in_proj columns it needs (z, x of its head, B, C, dt) -> bf16; causal
+//                    depthwise conv update (4 taps, fp32 math, SiLU, bf16 out) for its x channels
+//                    and for B/C; the SSM state update h = exp(dt A) h + (B dt) x with the bf16
+//                    state [headdim][d_state] streamed once (read + write, 16 KB per head);
+//                    y = C.h + D x -> bf16 -> y * silu(z) (fp32) for the gated RMSNorm.
+//                    The conv state is double-buffered by step parity (B/C channels are read by
+//                    every head's workgroup and rewritten by head 0's).
+//   k_mamba_conv_seq / k_mamba_scan : prefill. Causal conv over the whole prefix (parallel),
+//                    then the exact recurrence per (head, row), LDS-staged 16 steps at a time,
+//                    the fp32 state in registers; final state stored bf16.
+//   k_gated_norm   : RMSNormGated(norm_before_gate=False): out = bf16(g * rsqrt(mean(g^2)+eps) * w)
+//                    over the d_inner channels of a row (g = y * silu(z) from the kernels above).
+// The state update is HBM-bound: per decode step and Mamba layer 2 * R * d_inner * d_state * 2 B.
+#include "common.h"
+#include "../../include/zonos_hip.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int MB_THREADS = 256;
+constexpr int MB_MAXGS = 8;
+
+ZK_DEV float silu_f(float v) { return v / (1.0f + expf(-v)); }
+ZK_DEV float softplus_thr(float v) { return v <= 20.0f ? log1pf(expf(v)) : v; }
+
+// sum of the split-K slabs of one in_proj column, rounded to bf16 (the GEMM output dtype)
+ZK_DEV float slab_col(const float* p, size_t slab, int gs, int col) {
+    float v[MB_MAXGS];
+#pragma unroll
+    for (int s = 0; s < MB_MAXGS; ++s) v[s] = p[(size_t)min(s, gs - 1) * slab + col];
+    float a = v[0];
+#pragma unroll
+    for (int s = 1; s < MB_MAXGS; ++s)
+        if (s < gs) a += v[s];
+    return round_bf(a);
+}
+
+template <int HP, int DS>
+__global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
+    const float* __restrict__ part, int gs, int R, int di, int nh, const float* __restrict__ conv_w,
+    const float* __restrict__ conv_b, const bf16_t* __restrict__ cs_a, bf16_t* __restrict__ cs_b,
+    const int32_t* __restrict__ pos_dev, bf16_t* __restrict__ ssm, const float* __restrict__ A,
+    const float* __restrict__ dt_bias, const float* __restrict__ Dv, float* __restrict__ yz,
+    const int32_t* __restrict__ skip) {
+    constexpr int TPP = MB_THREADS / HP;     // threads per headdim row
+    constexpr int EPT = DS / TPP;            // state elements per thread
+    static_assert(TPP * HP == MB_THREADS && EPT * TPP == DS && EPT % 8 == 0, "tile");
+    __shared__ float s_x[HP], s_z[HP], s_B[DS], s_C[DS], s_dt;
+    if (skip && *skip) return;
+    const int h = blockIdx.x, r = blockIdx.y;
+    const int conv_dim = di + 2 * DS;
+    const int ncol = 2 * di + 2 * DS + nh;
+    const size_t slab = (size_t)R * ncol;
+    const float* prow = part + (size_t)r * ncol;
+    // conv state parity: step at position pos reads buffer (pos & 1), writes the other
+    const int par = pos_dev ? (*pos_dev & 1) : 0;
+    const bf16_t* csi = (par ? cs_b : cs_a) + (size_t)r * conv_dim * 4;
+    bf16_t* cso = (par ? const_cast<bf16_t*>(cs_a) : cs_b) + (size_t)r * conv_dim * 4;
+
+    for (int i = threadIdx.x; i < HP + 2 * DS + HP + 1; i += MB_THREADS) {
+        if (i < HP + 2 * DS) {
+            // conv channel: x channel of this head, or B / C
+            const int ch = i < HP ? h * HP + i : di + (i - HP);
+            const float xnew = slab_col(prow, slab, gs, di + ch);
+            const uint2 st = *reinterpret_cast<const uint2*>(csi + (size_t)ch * 4);
+            const float s1 = __uint_as_float((st.x >> 16) << 16), s2 = __uint_as_float((st.y & 0xffffu) << 16);
+            const float s3 = __uint_as_float((st.y >> 16) << 16);
+            const float* w = conv_w + (size_t)ch * 4;
+            float acc = conv_b[ch];
+            acc += w[0] * s1;
+            acc += w[1] * s2;
+            acc += w[2] * s3;
+            acc += w[3] * xnew;
+            const float o = round_bf(silu_f(acc));
+            if (i < HP) s_x[i] = o;
+            else if (i < HP + DS) s_B[i - HP] = o;
+            else s_C[i - HP - DS] = o;
+            if (i < HP || h == 0) {
+                const uint32_t lo = (st.x >> 16) | (st.y << 16);                       // s1, s2
+                const uint32_t hi = (st.y >> 16) | ((uint32_t)f2bf(xnew) << 16);        // s3, xnew
+                *reinterpret_cast<uint2*>(cso + (size_t)ch * 4) = make_uint2(lo, hi);
+            }
+        } else if (i < HP + 2 * DS + HP) {
+            const int j = i - HP - 2 * DS;
+            s_z[j] = slab_col(prow, slab, gs, h * HP + j);
+        } else {
+            s_dt = slab_col(prow, slab, gs, 2 * di + 2 * DS + h);
+        }
+    }
+    __syncthreads();
+    const int t = threadIdx.x, p = t / TPP, n0 = (t % TPP) * EPT;
+    const float dt = softplus_thr(s_dt + dt_bias[h]);
+    const float dA = expf(dt * A[h]);
+    const float xp = s_x[p];
+    bf16_t* sp = ssm + (((size_t)r * nh + h) * HP + p) * DS + n0;
+    float acc = 0.f;
+#pragma unroll
+    for (int e8 = 0; e8 < EPT; e8 += 8) {
+        float sv[8];
+        unpack8(*reinterpret_cast<const uint4*>(sp + e8), sv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int n = n0 + e8 + e;
+            const float s = sv[e] * dA + (s_B[n] * dt) * xp;
+            sv[e] = s;
+            acc += s * s_C[n];
+        }
+        *reinterpret_cast<uint4*>(sp + e8) = pack8(sv);
+    }
+#pragma unroll
+    for (int off = 1; off < TPP; off <<= 1) acc += __shfl_xor(acc, off, 64);
+    if (t % TPP == 0) {
+        const float y = round_bf(acc + xp * Dv[h]);
+        const float zz = s_z[p];
+        yz[(size_t)r * di + h * HP + p] = y * (zz * (1.0f / (1.0f + expf(-zz))));
+    }
+}
+
+// prefill conv: xc[r][t][ch] = bf16(silu(b + sum_k w[k] in[t-3+k])), in = bf16(in_proj xBC column);
+// final_state[r][ch] = last 4 inputs (zero-padded) -> the buffer the first decode step reads
+__global__ __launch_bounds__(MB_THREADS) void k_mamba_conv_seq(const float* __restrict__ zx, int S, int di, int ds,
+                                                               int nh, const float* __restrict__ conv_w,
+                                                               const float* __restrict__ conv_b,
+                                                               bf16_t* __restrict__ xc, bf16_t* __restrict__ cs) {
+    const int conv_dim = di + 2 * ds, ncol = 2 * di + 2 * ds + nh;
+    const int r = blockIdx.y;
+    const long idx = (long)blockIdx.x * MB_THREADS + threadIdx.x;
+    if (idx >= (long)(S + 1) * conv_dim) return;
+    const int ch = (int)(idx % conv_dim);
+    const int t = (int)(idx / conv_dim);
+    const float* base = zx + (size_t)r * S * ncol + di + ch;
+    auto in = [&](int u) -> float { return (u >= 0 && u < S) ? round_bf(base[(size_t)u * ncol]) : 0.f; };
+    if (t < S) {
+        const float* w = conv_w + (size_t)ch * 4;
+        float acc = conv_b[ch];
+        acc += w[0] * in(t - 3);
+        acc += w[1] * in(t - 2);
+        acc += w[2] * in(t - 1);
+        acc += w[3] * in(t);
+        xc[((size_t)r * S + t) * conv_dim + ch] = f2bf(silu_f(acc));
+    } else {
+        const uint32_t lo = (uint32_t)f2bf(in(S - 4)) | ((uint32_t)f2bf(in(S - 3)) << 16);
+        const uint32_t hi = (uint32_t)f2bf(in(S - 2)) | ((uint32_t)f2bf(in(S - 1)) << 16);
+        *reinterpret_cast<uint2*>(cs + ((size_t)r * conv_dim + ch) * 4) = make_uint2(lo, hi);
+    }
+}
+
+template <int HP, int DS>
+__global__ __launch_bounds__(MB_THREADS) void k_mamba_scan(const float* __restrict__ zx, const bf16_t* __restrict__ xc,
+                                                           int S, int di, int nh, const float* __restrict__ A,
+                                                           const float* __restrict__ dt_bias,
+                                                           const float* __restrict__ Dv, bf16_t* __restrict__ ssm,
+                                                           float* __restrict__ yz) {
+    constexpr int TPP = MB_THREADS / HP, EPT = DS / TPP, TC = 16;
+    __shared__ float s_x[TC][HP], s_z[TC][HP], s_B[TC][DS], s_C[TC][DS], s_dt[TC];
+    const int h = blockIdx.x, r = blockIdx.y;
+    const int conv_dim = di + 2 * DS, ncol = 2 * di + 2 * DS + nh;
+    const int t = threadIdx.x, p = t / TPP, n0 = (t % TPP) * EPT;
+    const float Ah = A[h], dtb = dt_bias[h], Dh = Dv[h];
+    float st[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) st[e] = 0.f;
+    for (int c0 = 0; c0 < S; c0 += TC) {
+        const int nt = min(TC, S - c0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nt * (2 * HP + 2 * DS + 1); i += MB_THREADS) {
+            const int tt = i / (2 * HP + 2 * DS + 1), k = i % (2 * HP + 2 * DS + 1);
+            const size_t row = (size_t)r * S + c0 + tt;
+            const bf16_t* xr = xc + row * conv_dim;
+            if (k < HP) s_x[tt][k] = bf2f(xr[h * HP + k]);
+            else if (k < HP + DS) s_B[tt][k - HP] = bf2f(xr[di + (k - HP)]);
+            else if (k < HP + 2 * DS) s_C[tt][k - HP - DS] = bf2f(xr[di + DS + (k - HP - DS)]);
+            else if (k < 2 * HP + 2 * DS) s_z[tt][k - HP - 2 * DS] = round_bf(zx[row * ncol + h * HP + (k - HP - 2 * DS)]);
+            else s_dt[tt] = round_bf(zx[row * ncol + 2 * di + 2 * DS + h]);
+        }
+        __syncthreads();
+        for (int tt = 0; tt < nt; ++tt) {
+            const float dt = softplus_thr(s_dt[tt] + dtb);
+            const float dA = expf(dt * Ah);
+            const float xp = s_x[tt][p];
+            float acc = 0.f;
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+                const int n = n0 + e;
+                st[e] = st[e] * dA + (s_B[tt][n] * dt) * xp;
+                acc += st[e] * s_C[tt][n];
+            }
+#pragma unroll
+            for (int off = 1; off < TPP; off <<= 1) acc += __shfl_xor(acc, off, 64);
+            if (t % TPP == 0) {
+                const float y = round_bf(acc + xp * Dh);
+                const float zz = s_z[tt][p];
+                yz[((size_t)r * S + c0 + tt) * di + h * HP + p] = y * (zz * (1.0f / (1.0f + expf(-zz))));
+            }
+        }
+    }
+    bf16_t* sp = ssm + (((size_t)r * nh + h) * HP + p) * DS + n0;
+#pragma unroll
+    for (int e8 = 0; e8 < EPT; e8 += 8) *reinterpret_cast<uint4*>(sp + e8) = pack8(st + e8);
+}
+
+__global__ __launch_bounds__(MB_THREADS) void k_gated_norm(const float* __restrict__ g, int di,
+                                                           const float* __restrict__ w, float eps,
+                                                           bf16_t* __restrict__ out, const int32_t* __restrict__ skip) {
+    __shared__ float red[MB_THREADS / 64];
+    if (skip && *skip) return;
+    const int row = blockIdx.x;
+    const float* gr = g + (size_t)row * di;
+    float s = 0.f;
+    for (int j = threadIdx.x; j < di; j += MB_THREADS) s += gr[j] * gr[j];
+    s = block_sum<MB_THREADS>(s, red);
+    const float rstd = 1.0f / sqrtf(s / (float)di + eps);
+    for (int j = threadIdx.x; j < di; j += MB_THREADS) out[(size_t)row * di + j] = f2bf((gr[j] * rstd) * w[j]);
+}
+
+}  // namespace
+
+#define ZK_MB_DISPATCH(HP_, DS_, CALL)                                                     \
+    if (hp == HP_ && ds == DS_) { CALL(HP_, DS_); handled = true; }
+
+extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
+                             int d_state, const float* conv_w, const float* conv_b, void* conv_state_a,
+                             void* conv_state_b, const int32_t* pos_dev, void* ssm_state, const float* A,
+                             const float* dt_bias, const float* D, float* yz, const int32_t* skip, void* stream) {
+    const int hp = headdim, ds = d_state;
+    ZK_REQUIRE(gemm_nsplit >= 1 && gemm_nsplit <= MB_MAXGS, "zk_mamba_step: gemm_nsplit=%d", gemm_nsplit);
+    ZK_REQUIRE(nheads * headdim == d_inner, "zk_mamba_step: nheads*headdim != d_inner");
+    bool handled = false;
+#define ZK_MB_STEP(HP_, DS_)                                                                                       \
+    hipLaunchKernelGGL((k_mamba_step<HP_, DS_>), dim3(nheads, R), dim3(MB_THREADS), 0, (hipStream_t)stream, part,  \
+                       gemm_nsplit, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,                \
+                       (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip)
+    ZK_MB_DISPATCH(64, 128, ZK_MB_STEP)
+    ZK_MB_DISPATCH(32, 64, ZK_MB_STEP)
+    ZK_MB_DISPATCH(64, 64, ZK_MB_STEP)
+#undef ZK_MB_STEP
+    ZK_REQUIRE(handled, "zk_mamba_step: (headdim %d, d_state %d) not instantiated", hp, ds);
+    ZK_CHECK_LAUNCH("zk_mamba_step");
+    return 0;
+}
+
+extern "C" int zk_mamba_prefill(const float* zx, int R, int S, int d_inner, int nheads, int headdim, int d_state,
+                                const float* conv_w, const float* conv_b, void* xc_scratch, void* conv_state,
+                                void* ssm_state, const float* A, const float* dt_bias, const float* D, float* yz,
+                                void* stream) {
+    const int hp = headdim, ds = d_state;
+    ZK_REQUIRE(nheads * headdim == d_inner && S >= 1, "zk_mamba_prefill: bad shape");
+    const int conv_dim = d_inner + 2 * d_state;
+    const long n = (long)(S + 1) * conv_dim;
+    hipLaunchKernelGGL(k_mamba_conv_seq, dim3((unsigned)((n + MB_THREADS - 1) / MB_THREADS), R), dim3(MB_THREADS), 0,
+                       (hipStream_t)stream, zx, S, d_inner, d_state, nheads, conv_w, conv_b, (bf16_t*)xc_scratch,
+                       (bf16_t*)conv_state);
+    ZK_CHECK_LAUNCH("zk_mamba_prefill/conv");
+    bool handled = false;
+#define ZK_MB_SCAN(HP_, DS_)                                                                                      \
+    hipLaunchKernelGGL((k_mamba_scan<HP_, DS_>), dim3(nheads, R), dim3(MB_THREADS), 0, (hipStream_t)stream, zx,   \
+                       (const bf16_t*)xc_scratch, S, d_inner, nheads, A, dt_bias, D, (bf16_t*)ssm_state, yz)
+    ZK_MB_DISPATCH(64, 128, ZK_MB_SCAN)
+    ZK_MB_DISPATCH(32, 64, ZK_MB_SCAN)
+    ZK_MB_DISPATCH(64, 64, ZK_MB_SCAN)
+#undef ZK_MB_SCAN
+    ZK_REQUIRE(handled, "zk_mamba_prefill: (headdim %d, d_state %d) not instantiated", hp, ds);
+    ZK_CHECK_LAUNCH("zk_mamba_prefill/scan");
+    return 0;
+}
+
+extern "C" int zk_gated_rmsnorm(const float* g, int rows, int d_inner, const float* w, float eps, void* out,
+                                const int32_t* skip, void* stream) {
+    ZK_REQUIRE(rows >= 0 && d_inner > 0, "zk_gated_rmsnorm: bad shape");
+    if (rows == 0) return 0;
+    hipLaunchKernelGGL(k_gated_norm, dim3(rows), dim3(MB_THREADS), 0, (hipStream_t)stream, g, d_inner, w, eps,
+                       (bf16_t*)out, skip);
+    ZK_CHECK_LAUNCH("zk_gated_rmsnorm");
+    return 0;
+}

@@ -96,6 +96,7 @@ class HipDecoder:
         _lib.load()
         self.cfg = cfg
         self.fuse_qkv = True      # in_proj epilogue inside the decode attention launch (False: separate kernel)
+        self.rope_neox = 0        # transformer: interleaved RoPE pairs (_torch.py:18-30)
         self.device = torch.device(device)
         c = cfg
         bf = torch.bfloat16
@@ -209,27 +210,28 @@ class HipDecoder:
             call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
             if prefill:
                 call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
-                     ptr(kc), ptr(vt), ws["smax"], ptr(ws["vrows"]), skip, stream)
+                     ptr(kc), ptr(vt), ws["smax"], ptr(ws["vrows"]), self.rope_neox, skip, stream)
                 call("zk_attn_prefill", ptr(q), ptr(kc), ptr(ws["vrows"]), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
             elif self.fuse_qkv:
                 # in_proj epilogue fused into the attention launch (position = ctx - 1 = scal[1])
                 call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
-                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), skip, stream)
+                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), self.rope_neox,
+                     skip, stream)
             else:
                 call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
-                     ptr(kc), ptr(vt), ws["smax"], None, skip, stream)
+                     ptr(kc), ptr(vt), ws["smax"], None, self.rope_neox, skip, stream)
                 call("zk_attn_decode", ptr(q), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1, ptr(scal[1:2]),
                      ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), skip, stream)
             call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip, stream)
             call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D, ptr(x),
-                 ptr(xn), skip, stream)
+                 ptr(xn), 0, skip, stream)
             call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fd, D, 1, 1, None, ptr(h), skip, stream)
             call("zk_gemm_bf16", ptr(h), Fd, ptr(L["fc2"]), M, D, Fd, sp["fc2"], 0, ptr(part), None, skip, stream)
             if i + 1 < len(self.layers):
                 nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
             else:
                 nw, nb = self.lnf_w, self.lnf_b
-            call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), skip,
+            call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 0, skip,
                  stream)
 
     def _heads(self, ws, R: int, S: int, stream, skip):

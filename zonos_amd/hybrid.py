@@ -1,0 +1,265 @@
+"""Hybrid (Mamba2 + attention) backbone on the MI355X engine: Zonos-v0.1-hybrid
+(zonos/backbone/_mamba_ssm.py:9-57 -> mamba_ssm create_block / Block / Mamba2 / MHA / GatedMLP).
+
+Same generate() machinery as the transformer engine (device-side step state, one hipGraph per
+decode step, shared embed / heads / sampler / EOS kernels); only the per-layer launch sequence
+differs:
+
+  Mamba2 layer : gemm(in_proj, split-K) -> mamba_step (slab reduce, conv update, SSM state
+                 update, y * silu(z)) -> gated_rmsnorm -> gemm(out_proj, split-K)
+                 -> resid_ln(ln_on_sum: fused add + LayerNorm of the fp32 sum)
+  attention    : gemm(Wqkv) -> attn_decode_qkv (GPT-NeoX RoPE, bf16 cos/sin cache)
+                 -> gemm(out_proj) -> resid_ln(norm2) -> gemm(fc1, SwiGLU) -> gemm(fc2) -> resid_ln
+
+State: per attention layer the KV cache (fragment order, zonos_amd.kvlayout); per Mamba layer the
+conv state (bf16 [R][conv_dim][4], double-buffered by step parity) and the SSM state (bf16
+[R][nheads][headdim][d_state], as Zonos allocates the inference cache in bf16, model.py:204-208).
+Prefill runs the causal conv over the prefix and the exact recurrence (zk_mamba_prefill).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+from .engine import ATTN_CHUNK, N_CB, VOCAB, HipDecoder, _split_for, attn_splits_for, pack_weights
+
+
+@dataclass
+class HybridEngineConfig:
+    d_model: int
+    n_layer: int
+    attn_layer_idx: tuple
+    n_heads: int
+    n_kv: int
+    d_ff: int
+    d_state: int = 128
+    d_conv: int = 4
+    expand: int = 2
+    headdim: int = 64
+    ngroups: int = 1
+    rotary_base: float = 10000.0
+    eps: float = 1e-5
+
+    @property
+    def head_dim(self):
+        return self.d_model // self.n_heads
+
+    @property
+    def d_inner(self):
+        return self.expand * self.d_model
+
+    @property
+    def nheads_ssm(self):
+        return self.d_inner // self.headdim
+
+    @property
+    def conv_dim(self):
+        return self.d_inner + 2 * self.ngroups * self.d_state
+
+    @property
+    def d_in_proj(self):
+        return 2 * self.d_inner + 2 * self.ngroups * self.d_state + self.nheads_ssm
+
+    @classmethod
+    def from_backbone_config(cls, bc) -> "HybridEngineConfig":
+        """zonos.config.BackboneConfig of a hybrid checkpoint (mamba_ssm create_block arguments)."""
+        a, s = dict(bc.attn_cfg or {}), dict(bc.ssm_cfg or {})
+        if s.pop("layer", "Mamba2") != "Mamba2":
+            raise ValueError("only Mamba2 SSM layers are supported")
+        if a.get("qkv_proj_bias", False) or a.get("out_proj_bias", False):
+            raise ValueError("biased attention projections are not supported")
+        if bc.d_intermediate != 0 or bc.rms_norm or bc.residual_in_fp32:
+            raise ValueError("hybrid variant not supported (d_intermediate / rms_norm / residual_in_fp32)")
+        if a.get("rotary_emb_dim", bc.d_model // a.get("num_heads", 16)) != bc.d_model // a.get("num_heads", 16):
+            raise ValueError("partial rotary embeddings are not supported")
+        return cls(d_model=bc.d_model, n_layer=bc.n_layer, attn_layer_idx=tuple(bc.attn_layer_idx),
+                   n_heads=a.get("num_heads", 16), n_kv=a.get("num_heads_kv", a.get("num_heads", 16)),
+                   d_ff=bc.attn_mlp_d_intermediate, d_state=s.get("d_state", 128), d_conv=s.get("d_conv", 4),
+                   expand=s.get("expand", 2), headdim=s.get("headdim", 64), ngroups=s.get("ngroups", 1),
+                   rotary_base=a.get("rotary_emb_base", 10000.0), eps=bc.norm_epsilon)
+
+
+def rotary_table(seq_len: int, dim: int, base: float = 10000.0) -> torch.Tensor:
+    """flash_attn RotaryEmbedding cos/sin cache (fp32 math, cached in bf16 as the model dtype),
+    returned as fp32 [seq_len][dim/2][2] holding the bf16-rounded values."""
+    inv = 1.0 / (base ** (torch.arange(0, dim, 2, dtype=torch.float32) / dim))
+    f = torch.outer(torch.arange(seq_len, dtype=torch.float32), inv)
+    return torch.stack([torch.cos(f).to(torch.bfloat16).float(), torch.sin(f).to(torch.bfloat16).float()],
+                       dim=-1).contiguous()
+
+
+class HybridDecoder(HipDecoder):
+    """generate() for the hybrid backbone (the layer loop and state differ from HipDecoder)."""
+
+    def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda"):
+        _lib.load()
+        if cfg.d_conv != 4 or cfg.ngroups != 1:
+            raise ValueError("Mamba2 d_conv=4, ngroups=1 only")
+        self.cfg = cfg
+        self.fuse_qkv = True
+        self.rope_neox = 1
+        self.device = torch.device(device)
+        dev, bf = self.device, torch.bfloat16
+
+        def w(name):
+            return weights[name].to(device=dev, dtype=bf).contiguous()
+
+        def f32(name):
+            return weights[name].to(device=dev, dtype=bf).float().contiguous()
+
+        stream = _lib.stream_ptr(dev)
+        self.emb = torch.stack([w(f"embeddings.{k}.weight") for k in range(N_CB)]).contiguous()
+        heads = []
+        for k in range(N_CB):
+            h = w(f"heads.{k}.weight")
+            if h.shape[0] < VOCAB:
+                h = torch.cat([h, h.new_zeros(VOCAB - h.shape[0], h.shape[1])])
+            heads.append(h)
+        self.heads = pack_weights(torch.cat(heads).contiguous(), stream)
+        self.layers = []
+        for i in range(cfg.n_layer):
+            p = f"backbone.layers.{i}."
+            L = dict(ln1_w=w(p + "norm.weight"), ln1_b=w(p + "norm.bias"))
+            if i in cfg.attn_layer_idx:
+                fc1 = w(p + "mlp.fc1.weight")
+                fc1p = torch.empty_like(fc1)
+                call("zk_permute_fc1", ptr(fc1), cfg.d_ff, cfg.d_model, ptr(fc1p), stream)
+                L.update(type="attn", wqkv=pack_weights(w(p + "mixer.in_proj.weight"), stream),
+                         wo=pack_weights(w(p + "mixer.out_proj.weight"), stream),
+                         ln2_w=w(p + "norm2.weight"), ln2_b=w(p + "norm2.bias"),
+                         fc1=pack_weights(fc1p, stream), fc2=pack_weights(w(p + "mlp.fc2.weight"), stream))
+            else:
+                cw = weights[p + "mixer.conv1d.weight"].to(device=dev, dtype=bf).float()
+                L.update(type="mamba", w_in=pack_weights(w(p + "mixer.in_proj.weight"), stream),
+                         conv_w=cw.reshape(cfg.conv_dim, cfg.d_conv).contiguous(),
+                         conv_b=f32(p + "mixer.conv1d.bias"),
+                         A=(-torch.exp(weights[p + "mixer.A_log"].to(bf).float())).to(dev).contiguous(),
+                         dt_bias=f32(p + "mixer.dt_bias"), D=f32(p + "mixer.D"),
+                         norm_w=f32(p + "mixer.norm.weight"),
+                         w_out=pack_weights(w(p + "mixer.out_proj.weight"), stream))
+            self.layers.append(L)
+        self.attn_ids = [i for i in range(cfg.n_layer) if i in cfg.attn_layer_idx]
+        self.mamba_ids = [i for i in range(cfg.n_layer) if i not in cfg.attn_layer_idx]
+        self.lnf_w = w("backbone.norm_f.weight")
+        self.lnf_b = w("backbone.norm_f.bias")
+        self.freqs = rotary_table(16384, cfg.head_dim, cfg.rotary_base).to(dev)
+        self._ws = None
+        torch.cuda.synchronize(dev)
+
+    # ------------------------------------------------------------------ workspace
+    def _alloc(self, B: int, Lc: int, P: int, max_new: int) -> dict:
+        c = self.cfg
+        dev = self.device
+        R = 2 * B
+        T = P + max_new
+        Ld = T + N_CB
+        seq_len = Lc + T + N_CB
+        smax = -(-seq_len // ATTN_CHUNK) * ATTN_CHUNK
+        S_pre = Lc + P + 1
+        key = (B, Lc, P, max_new)
+        if self._ws is not None and self._ws["key"] == key:
+            ws = self._ws
+            ws["kv"].zero_()
+            ws["conv"].zero_()
+            ws["ssm"].zero_()
+            return ws
+        self.release()
+        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+        di, nin = c.d_inner, c.d_in_proj
+        Nqkv = (H + 2 * Hk) * hd
+        Nh = N_CB * VOCAB
+        Mp = R * S_pre
+        f32, bf, i32 = torch.float32, torch.bfloat16, torch.int32
+        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R), fc2=_split_for(D, max(Fd, 64), R),
+                      heads=_split_for(Nh, D, R), inp=min(_split_for(nin, D, R), 8), out=_split_for(D, di, R))
+        part_n = max(Mp * Nqkv, Mp * D, Mp * nin, splits["qkv"] * R * Nqkv, splits["o"] * R * D,
+                     splits["fc2"] * R * D, splits["heads"] * R * Nh, splits["inp"] * R * nin, splits["out"] * R * D)
+        attn_splits = attn_splits_for(R, Hk, smax)
+        na, nm = len(self.attn_ids), len(self.mamba_ids)
+        ws = dict(
+            key=key, R=R, T=T, Ld=Ld, smax=smax, S_pre=S_pre, splits=splits, attn_splits=attn_splits,
+            kv=torch.zeros(max(na, 1), 2, R * Hk * smax * hd, dtype=bf, device=dev),
+            conv=torch.zeros(max(nm, 1), 2, R * c.conv_dim * 4, dtype=bf, device=dev),
+            ssm=torch.zeros(max(nm, 1), R * c.nheads_ssm * c.headdim * c.d_state, dtype=bf, device=dev),
+            x=torch.empty(Mp, D, dtype=bf, device=dev), xn=torch.empty(Mp, D, dtype=bf, device=dev),
+            q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
+            h=torch.empty(Mp, max(Fd, 1), dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
+            yz=torch.empty(Mp, di, dtype=f32, device=dev), ym=torch.empty(Mp, di, dtype=bf, device=dev),
+            xc=torch.empty(Mp, c.conv_dim, dtype=bf, device=dev),
+            vrows=torch.empty(R * Hk * S_pre * hd, dtype=bf, device=dev),
+            attn_work=torch.empty(max(1, R * Hk * attn_splits * (8 + 4 * hd)), dtype=f32, device=dev),
+            scal=torch.zeros(16, dtype=i32, device=dev),
+            eos_mode=torch.zeros(B, dtype=i32, device=dev), steps_after=torch.zeros(B, dtype=i32, device=dev),
+            remaining=torch.zeros(B, dtype=i32, device=dev), stopping=torch.zeros(B, dtype=i32, device=dev),
+            act=torch.zeros(B, dtype=i32, device=dev), rp=torch.ones(B, dtype=f32, device=dev),
+            tok0=torch.zeros(B * N_CB, dtype=i32, device=dev), tok1=torch.zeros(B * N_CB, dtype=i32, device=dev),
+            delayed=torch.empty(B, N_CB, Ld, dtype=torch.int64, device=dev),
+            dbg=torch.empty(B, N_CB, VOCAB, dtype=f32, device=dev),
+            graph=None,
+        )
+        self._ws = ws
+        return ws
+
+    def _kv(self, ws, layer):
+        j = self.attn_ids.index(layer)
+        return ws["kv"][j, 0], ws["kv"][j, 1]
+
+    # ------------------------------------------------------------------ layer loop
+    def _layers(self, ws, M: int, R: int, S: int, prefill: bool, stream, skip):
+        c = self.cfg
+        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+        di, nin, nh = c.d_inner, c.d_in_proj, c.nheads_ssm
+        Nqkv = (H + 2 * Hk) * hd
+        sp = ws["splits"] if not prefill else dict(qkv=1, o=1, fc2=1, inp=1, out=1)
+        x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
+        scal = ws["scal"]
+        pos_dev = None if prefill else ptr(scal[1:2])
+        for i, L in enumerate(self.layers):
+            if i + 1 < len(self.layers):
+                nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
+            else:
+                nw, nb = self.lnf_w, self.lnf_b
+            if L["type"] == "attn":
+                kc, vt = self._kv(ws, i)
+                call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip,
+                     stream)
+                if prefill:
+                    call("zk_qkv_rope", ptr(part), 1, R, S, H, Hk, hd, ptr(self.freqs), 0, None, ptr(q), ptr(kc),
+                         ptr(vt), ws["smax"], ptr(ws["vrows"]), 1, skip, stream)
+                    call("zk_attn_prefill", ptr(q), ptr(kc), ptr(ws["vrows"]), R, S, H, Hk, hd, ws["smax"], ptr(y),
+                         stream)
+                else:
+                    call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                         ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), 1, skip,
+                         stream)
+                call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip,
+                     stream)
+                call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D,
+                     ptr(x), ptr(xn), 1, skip, stream)
+                call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fd, D, 1, 1, None, ptr(h), skip, stream)
+                call("zk_gemm_bf16", ptr(h), Fd, ptr(L["fc2"]), M, D, Fd, sp["fc2"], 0, ptr(part), None, skip, stream)
+                call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 1,
+                     skip, stream)
+            else:
+                j = self.mamba_ids.index(i)
+                conv, ssm = ws["conv"][j], ws["ssm"][j]
+                call("zk_gemm_bf16", ptr(xn), D, ptr(L["w_in"]), M, nin, D, sp["inp"], 0, ptr(part), None, skip,
+                     stream)
+                if prefill:
+                    # the first decode step (position S) reads conv buffer (S & 1)
+                    call("zk_mamba_prefill", ptr(part), R, S, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
+                         ptr(L["conv_b"]), ptr(ws["xc"]), ptr(conv[S & 1]), ptr(ssm), ptr(L["A"]), ptr(L["dt_bias"]),
+                         ptr(L["D"]), ptr(ws["yz"]), stream)
+                else:
+                    call("zk_mamba_step", ptr(part), sp["inp"], R, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
+                         ptr(L["conv_b"]), ptr(conv[0]), ptr(conv[1]), pos_dev, ptr(ssm), ptr(L["A"]),
+                         ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), skip, stream)
+                call("zk_gated_rmsnorm", ptr(ws["yz"]), M, di, ptr(L["norm_w"]), 1e-5, ptr(ws["ym"]), skip, stream)
+                call("zk_gemm_bf16", ptr(ws["ym"]), di, ptr(L["w_out"]), M, D, di, sp["out"], 0, ptr(part), None,
+                     skip, stream)
+                call("zk_resid_ln", ptr(part), sp["out"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 1,
+                     skip, stream)

@@ -20,16 +20,25 @@ from .engine import EngineConfig, HipDecoder
 from .utils import DEFAULT_DEVICE, hub_download
 
 
+def is_hybrid(bc) -> bool:
+    """A backbone with SSM layers (ssm_cfg set and some layer not in attn_layer_idx)."""
+    return bool(bc.ssm_cfg) and len(set(bc.attn_layer_idx or [])) < bc.n_layer
+
+
 class Zonos:
     def __init__(self, config: ZonosConfig, state_dict: dict, device=DEFAULT_DEVICE,
                  autoencoder: DACAutoencoder | None = None):
-        if config.backbone.ssm_cfg:
-            raise NotImplementedError("the hybrid (Mamba2) backbone is not implemented by the HIP engine yet")
         self.config = config
         self.eos_token_id = config.eos_token_id
         self.masked_token_id = config.masked_token_id
         self.device = torch.device(device)
-        self.engine = HipDecoder(EngineConfig.from_backbone_config(config.backbone), state_dict, self.device)
+        bc = config.backbone
+        if is_hybrid(bc):
+            # Zonos-v0.1-hybrid: mamba_ssm backbone (zonos/backbone/_mamba_ssm.py)
+            from .hybrid import HybridDecoder, HybridEngineConfig
+            self.engine = HybridDecoder(HybridEngineConfig.from_backbone_config(bc), state_dict, self.device)
+        else:
+            self.engine = HipDecoder(EngineConfig.from_backbone_config(bc), state_dict, self.device)
         self._autoencoder = autoencoder
 
     @property
