@@ -43,7 +43,9 @@ def parse():
     ap.add_argument("--lc", type=int, default=400)
     ap.add_argument("--prefix", type=int, default=10)
     ap.add_argument("--new-tokens", type=int, default=2580)
-    ap.add_argument("--layers", type=int, default=26)
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--model", choices=["transformer", "hybrid"], default="transformer",
+                    help="hybrid = Zonos-v0.1-hybrid geometry as assumed in synthetic.ZONOS_V01_HYBRID (config 5)")
     ap.add_argument("--no-dac", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=1)
@@ -71,7 +73,7 @@ def attn_roofline(eng, ctx, reps=50):
     call("zk_event_create", C.byref(e0))
     call("zk_event_create", C.byref(e1))
     args = (ptr(ws["part"]), gs, ptr(eng.freqs), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], ctx, None,
-            ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["y"]), None, stream)
+            ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["y"]), 0, None, stream)
     for _ in range(5):
         call("zk_attn_decode_qkv", *args)
     call("zk_event_record", e0.value, stream)
@@ -88,7 +90,7 @@ def attn_roofline(eng, ctx, reps=50):
     ach = bytes_per_launch / per_launch_s / 1e9
     traffic = None
     import glob
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*attn_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*attn*pmc*.json"))):
         d = json.load(open(f))
         if d.get("R") == R and d.get("ctx") == ctx and d.get("kernel") == "k_attn_decode<true>":
             traffic = d["hbm_bytes_per_launch"]
@@ -97,6 +99,43 @@ def attn_roofline(eng, ctx, reps=50):
                 ("+k_attn_combine" if ws["attn_splits"] > 1 else ""),
                 ctx=ctx, attn_splits=ws["attn_splits"],
                 bytes_per_launch=bytes_per_launch, us_per_launch=round(per_launch_s * 1e6, 2))
+
+
+def mamba_roofline(eng, reps=50):
+    """Hybrid: time zk_mamba_step (the SSM state update, HBM-bound) of one Mamba layer with HIP
+    events; algorithmic bytes = SSM state read + write (R*d_inner*d_state*2 B each) + conv
+    state read + write + in_proj slabs read + yz write."""
+    import ctypes as C
+
+    from zonos_amd import _lib
+    from zonos_amd._lib import call, ptr
+    ws, c = eng._ws, eng.cfg
+    R = ws["R"]
+    j = len(eng.mamba_ids) // 2
+    L = eng.layers[eng.mamba_ids[j]]
+    stream = _lib.stream_ptr()
+    e0, e1 = _lib.P(), _lib.P()
+    call("zk_event_create", C.byref(e0))
+    call("zk_event_create", C.byref(e1))
+    gs = ws["splits"]["inp"]
+    args = (ptr(ws["part"]), gs, R, c.d_inner, c.nheads_ssm, c.headdim, c.d_state, ptr(L["conv_w"]),
+            ptr(L["conv_b"]), ptr(ws["conv"][j][0]), ptr(ws["conv"][j][1]), ptr(ws["scal"][1:2]), ptr(ws["ssm"][j]),
+            ptr(L["A"]), ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), None, stream)
+    for _ in range(5):
+        call("zk_mamba_step", *args)
+    call("zk_event_record", e0.value, stream)
+    for _ in range(reps):
+        call("zk_mamba_step", *args)
+    call("zk_event_record", e1.value, stream)
+    ms = C.c_float()
+    call("zk_event_elapsed_ms", e0.value, e1.value, C.byref(ms))
+    call("zk_event_destroy", e0.value)
+    call("zk_event_destroy", e1.value)
+    per = ms.value / 1e3 / reps
+    b = (R * c.d_inner * c.d_state * 2 * 2 + R * c.conv_dim * 8 * 2 + gs * R * c.d_in_proj * 4 + R * c.d_inner * 4)
+    ach = b / per / 1e9
+    return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
+                traffic=None, kernel="k_mamba_step", bytes_per_launch=b, us_per_launch=round(per * 1e6, 2))
 
 
 def cpu_baseline(args):
@@ -164,9 +203,18 @@ def main():
     from zonos_amd.autoencoder import DacSpec, HipDacDecoder
     from zonos_amd.engine import EngineConfig, HipDecoder
 
-    mc = dict(synthetic.ZONOS_V01, n_layer=args.layers)
-    W = synthetic.backbone_weights(dev, seed=0, **mc)
-    eng = HipDecoder(EngineConfig(**mc), W, dev)
+    if args.model == "hybrid":
+        from zonos_amd.hybrid import HybridDecoder, HybridEngineConfig
+        mc = dict(synthetic.ZONOS_V01_HYBRID)
+        if args.layers:
+            mc["n_layer"] = args.layers
+            mc["attn_layer_idx"] = tuple(i for i in mc["attn_layer_idx"] if i < args.layers)
+        W = synthetic.hybrid_weights(dev, seed=0, **mc)
+        eng = HybridDecoder(HybridEngineConfig(**mc), W, dev)
+    else:
+        mc = dict(synthetic.ZONOS_V01, n_layer=args.layers or 26)
+        W = synthetic.backbone_weights(dev, seed=0, **mc)
+        eng = HipDecoder(EngineConfig(**mc), W, dev)
     del W
     dac = None if args.no_dac else HipDacDecoder(DacSpec(), synthetic.dac_weights(dev), dev)
     B = args.batch
@@ -219,16 +267,22 @@ def main():
         codes_s = frames * 9 / elapsed
         audio_s = frames / FRAME_RATE
         ctx_mean = args.lc + args.prefix + 1 + (args.new_tokens + 8) // 2
-        roof = attn_roofline(eng, ctx_mean)
+        roof = attn_roofline(eng, ctx_mean) if args.model == "transformer" else mamba_roofline(eng)
+        model = "Zonos-v0.1-transformer" if args.model == "transformer" else "Zonos-v0.1-hybrid (assumed geometry)"
+        cfg_name = {(64, 400, 10, 2580): "c3", (1, 160, 0, 861): "c2"}.get(
+            (args.batch, args.lc, args.prefix, args.new_tokens), "custom")
+        if args.model == "hybrid" and cfg_name == "c3":
+            cfg_name = "c5"
+        workload = (f"{cfg_name}: B={B}/GPU, Lc={args.lc}, prefix {args.prefix}, {args.new_tokens} new tokens "
+                    f"({args.new_tokens / FRAME_RATE:.0f} s), EOS disabled, CLI sampling (linear .65 conf .4 rep "
+                    f"2.5/8), DAC decode of all codes")
         out = {
-            "metric": "DAC codes/sec (end-to-end generate + DAC decode), Zonos-v0.1-transformer batch=64/GPU",
+            "metric": f"DAC codes/sec (end-to-end generate + DAC decode), {model} batch={B}/GPU",
             "value": round(codes_s, 1), "unit": "codes/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded random weights + LayerNorm'd random conditioning; no checkpoint offline)",
-            "config": {"workload": "c3: B=64/GPU, Lc=400, prefix 10, 2580 new tokens (30 s), EOS disabled, "
-                                   "CLI sampling (linear .65 conf .4 rep 2.5/8), DAC decode of all codes",
-                       "model": "Zonos-v0.1-transformer", "global_batch": B * world,
+            "config": {"workload": workload, "model": model, "global_batch": B * world,
                        "seq_len": args.lc + args.prefix + args.new_tokens + 9, "parallelism": f"dp{world}"},
             "rtf": round(audio_s / elapsed, 2),
             "breakdown": {"generate_s_per_step": round(stats["gen_s"] / args.steps, 3),
@@ -239,7 +293,7 @@ def main():
                                                             3)},
             "roofline": roof,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.model == "transformer":
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -52,6 +52,77 @@ def backbone_weights(device, seed=0, **cfg) -> dict:
     return W
 
 
+# Zonos-v0.1-hybrid geometry as assumed here (the hybrid config.json is not available offline;
+# mamba_ssm Mamba2 defaults for the SSM layers). Every size is a parameter.
+ZONOS_V01_HYBRID = dict(d_model=2048, n_layer=46, attn_layer_idx=(9, 18, 27, 36, 45), n_heads=16, n_kv=4,
+                        d_ff=8192, d_state=128, d_conv=4, expand=2, headdim=64)
+
+
+def hybrid_shapes(d_model, n_layer, attn_layer_idx, n_heads, n_kv, d_ff, d_state=128, d_conv=4, expand=2,
+                  headdim=64, n_cb=9, vocab=1026) -> dict:
+    """mamba_ssm parameter names (create_block: Mamba2 / MHA / GatedMLP, Block norms)."""
+    hd = d_model // n_heads
+    di = expand * d_model
+    nh = di // headdim
+    conv_dim = di + 2 * d_state
+    s = {}
+    for i in range(n_layer):
+        p = f"backbone.layers.{i}."
+        s[p + "norm.weight"] = (d_model,)
+        s[p + "norm.bias"] = (d_model,)
+        if i in attn_layer_idx:
+            s[p + "mixer.in_proj.weight"] = ((n_heads + 2 * n_kv) * hd, d_model)
+            s[p + "mixer.out_proj.weight"] = (d_model, n_heads * hd)
+            s[p + "norm2.weight"] = (d_model,)
+            s[p + "norm2.bias"] = (d_model,)
+            s[p + "mlp.fc1.weight"] = (2 * d_ff, d_model)
+            s[p + "mlp.fc2.weight"] = (d_model, d_ff)
+        else:
+            s[p + "mixer.in_proj.weight"] = (2 * di + 2 * d_state + nh, d_model)
+            s[p + "mixer.conv1d.weight"] = (conv_dim, 1, d_conv)
+            s[p + "mixer.conv1d.bias"] = (conv_dim,)
+            s[p + "mixer.dt_bias"] = (nh,)
+            s[p + "mixer.A_log"] = (nh,)
+            s[p + "mixer.D"] = (nh,)
+            s[p + "mixer.norm.weight"] = (di,)
+            s[p + "mixer.out_proj.weight"] = (d_model, di)
+    s["backbone.norm_f.weight"] = (d_model,)
+    s["backbone.norm_f.bias"] = (d_model,)
+    for k in range(n_cb):
+        s[f"embeddings.{k}.weight"] = (vocab, d_model)
+        s[f"heads.{k}.weight"] = (vocab - 1, d_model)
+    return s
+
+
+def hybrid_weights(device, seed=0, **cfg) -> dict:
+    """Seeded bf16 hybrid weights generated on the device (Mamba2's init ranges for A_log and dt)."""
+    c = dict(ZONOS_V01_HYBRID)
+    c.update(cfg)
+    g = torch.Generator(device=device).manual_seed(seed)
+    W = {}
+    for k, shape in hybrid_shapes(**c).items():
+        if k.endswith(("norm.weight", "norm2.weight", "norm_f.weight")):
+            t = 1.0 + 0.1 * torch.randn(shape, generator=g, device=device)
+        elif k.endswith("A_log"):
+            t = torch.log(1 + 15 * torch.rand(shape, generator=g, device=device))
+        elif k.endswith("dt_bias"):
+            dt = torch.exp(torch.rand(shape, generator=g, device=device) * (math.log(0.1) - math.log(1e-3))
+                           + math.log(1e-3))
+            t = dt + torch.log(-torch.expm1(-dt))
+        elif k.endswith(".D"):
+            t = torch.ones(shape, device=device)
+        elif k.endswith("conv1d.weight"):
+            t = torch.randn(shape, generator=g, device=device) / 2.0
+        elif k.endswith(".bias"):
+            t = 0.1 * torch.randn(shape, generator=g, device=device)
+        elif k.startswith("embeddings"):
+            t = torch.randn(shape, generator=g, device=device)
+        else:
+            t = torch.randn(shape, generator=g, device=device) / math.sqrt(shape[1])
+        W[k] = t.to(torch.bfloat16)
+    return W
+
+
 def dac_shapes(hidden=1024, dec=1536, ratios=(8, 8, 4, 2), ncb=9, ncode=1024, cdim=8) -> dict:
     s = {}
     for k in range(ncb):
