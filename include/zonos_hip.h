@@ -123,12 +123,12 @@ int zk_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv, int
  * decode: one query per row, keys [0, ctx) with ctx = ctx0 + *ctx_dev; flash-decoding
  *         over 128-key blocks split across `nsplit` workgroups per (row, kv head)
  *         (nsplit <= Smax/128; work: fp32 [R][Hkv][nsplit][8 + 4*hd] when nsplit > 1).
- * prefill: S queries per row at positions 0..S-1, causal (is_causal=S>1), V from v_rows.
+ * prefill: S queries per row at positions 0..S-1, causal (is_causal=S>1), K and V from the cache.
  * Output bf16 [rows][H*hd]. */
 int zk_attn_decode(const void* q, const void* k_cache, const void* vt_cache, int R, int H, int Hkv,
                    int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int nsplit,
                    void* out, const int32_t* skip, void* stream);
-int zk_attn_prefill(const void* q, const void* k_cache, const void* v_rows, int R, int S, int H,
+int zk_attn_prefill(const void* q, const void* k_cache, const void* vt_cache, int R, int S, int H,
                     int Hkv, int hd, int Smax, void* out, void* stream);
 /* Decode with the in_proj epilogue fused in (= zk_qkv_rope at pos = ctx-1, S = 1, followed by
  * zk_attn_decode): reduces the in_proj slabs (gemm_nsplit x [R][(H+2Hkv)*hd] fp32), applies

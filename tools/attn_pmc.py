@@ -28,7 +28,7 @@ work = torch.empty(1, device=dev)
 s = _lib.stream_ptr()
 for _ in range(20):
     call("zk_attn_decode_qkv", ptr(part), gsplit, ptr(freqs), ptr(kc), ptr(vt), R, H, Hk, hd, smax, ctx, None,
-         ptr(work), 1, ptr(out), None, s)
+         ptr(work), 1, ptr(out), 0, None, s)
 torch.cuda.synchronize()
 print(f"R={R} ctx={ctx} smax={smax}: 20 launches; algorithmic bytes/launch = "
       f"{R * ctx * Hk * hd * 4 + gsplit * R * N * 4 + R * H * hd * 2 + R * Hk * hd * 4}")

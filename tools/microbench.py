@@ -79,7 +79,7 @@ def attn():
             i = it[0] % ncopy
             it[0] += 1
             call("zk_attn_decode_qkv", ptr(part), gs, ptr(freqs), ptr(kcs[i]), ptr(vts[i]), R, H, Hk, hd, smax, ctx,
-                 None, ptr(work), 1, ptr(out), None, S)
+                 None, ptr(work), 1, ptr(out), 0, None, S)
         us = timeit(fq)
         b = R * ctx * Hk * hd * 2 * 2 + gs * R * (H + 2 * Hk) * hd * 4
         print(f"attn+qkv ctx={ctx:5d} fused: {us:8.1f} us  {b/1e6:7.1f} MB  {b / (us * 1e-6) / 1e9:7.0f} GB/s",
@@ -88,7 +88,7 @@ def attn():
 
         def fr():
             call("zk_qkv_rope", ptr(part), gs, R, 1, H, Hk, hd, ptr(freqs), ctx - 1, None, ptr(qkv_out), ptr(kcs[0]),
-                 ptr(vts[0]), smax, None, None, S)
+                 ptr(vts[0]), smax, None, 0, None, S)
         us = timeit(fr)
         print(f"qkv_rope alone ctx={ctx:5d}: {us:8.1f} us", flush=True)
 

@@ -8,7 +8,7 @@
 //                  -> q buffer + KV cache store (_torch.py:33-49).
 //   k_attn_decode: split-KV GQA decode attention on MFMA 16x16x32 bf16 (K on the A side,
 //                  the 4 query heads of a KV head on the B side), k_attn_combine merges splits.
-//   k_attn_prefill: causal prefill attention, one wave per query, 64-key chunks.
+//   k_attn_prefill: causal prefill attention on MFMA (16 queries per wave, two passes).
 //
 // KV cache layout: see "KV cache layout" below (32-key slices in MFMA-fragment order).
 #include "common.h"
@@ -549,62 +549,97 @@ __global__ __launch_bounds__(64) void k_attn_combine(const float* work, int H, i
 }
 
 // ------------------------------------------------------------------ prefill attention (causal)
-// One wave per query (r, h, t); 64-key chunks: lane = key for the scores, lane = 2 channels
-// for the output. K rows and V rows ([R][Hkv][S][hd] scratch written by k_qkv_rope) stream
-// coalesced.
-__global__ __launch_bounds__(256) void k_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vrows, int R,
+// MFMA form of the decode kernel's slice step with 16 QUERIES as the B operand: workgroup =
+// (64-query tile, head, row), each wave owns 16 queries and walks the 32-key slices of the
+// packed cache up to its last query (causal). Two passes like the reference's CPU flash kernel
+// on a single KV block: the exact row max first (S^T = K.Q^T), then p = exp(s - max) summed in
+// fp32 and rounded to bf16 for O^T = V^T.P^T. Each wave's queries are independent (no merge).
+__global__ __launch_bounds__(256) void k_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vt, int R,
                                                       int S, int H, int Hkv, int Smax, float scale, bf16_t* out) {
     constexpr int HD = 128;
-    __shared__ uint4 sq[4][HD / 8];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * 4 + w;          // query index within (r, h)
+    const int ln = lane & 15, lg = lane >> 4;
     const int h = blockIdx.y, r = blockIdx.z;
-    const bool active = qi < S;
-    const int t = active ? qi : S - 1;
+    const int q0 = blockIdx.x * 64 + w * 16;               // this wave's first query
+    if (q0 >= S) return;
     const int G = H / Hkv, g = h / G;
-    const bf16_t* qr = q + ((size_t)(r * S + t) * H + h) * HD;
-    if (lane < HD / 8) sq[w][lane] = reinterpret_cast<const uint4*>(qr)[lane];
-    __syncthreads();
+    const int qt = min(q0 + ln, S - 1);                     // query of this lane's B column
+    bf16x8 qf[4];
+    {
+        const bf16_t* qr = q + ((size_t)(r * S + qt) * H + h) * HD;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = as_frag(*reinterpret_cast<const uint4*>(qr + ks * 32 + lg * 8));
+    }
     const bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
-    const bf16_t* vb = vrows + ((size_t)r * Hkv + g) * S * HD;
-    // Two passes like the CPU flash kernel on a single KV block: exact row max first, then
-    // p = exp(s - max) summed in fp32 and rounded to bf16 for the P.V product.
-    auto score = [&](int key) -> float {
-        float acc = 0.f;
+    const bf16_t* vb = vt + ((size_t)r * Hkv + g) * Smax * HD;
+    const int last = min(q0 + 15, S - 1);                   // keys 0..last can be visible
+    const int nsl = last / 32 + 1;
+    // lane's 8 score values: keys 8lg .. 8lg+7 of the slice (tile h: 8lg + 4h + i), query qt
+    auto scores = [&](int sl, f32x4* sacc) {
+        const int lanei = lg * 16 + ln;
+        const bf16_t* k0 = kb + (size_t)sl * 4096 + lanei * 8;
 #pragma unroll
-        for (int i = 0; i < HD / 8; ++i) {
-            float a[8], bq[8];
-            unpack8(*reinterpret_cast<const uint4*>(kb + k_off(key, i)), a);
-            unpack8(sq[w][i], bq);
+        for (int t = 0; t < 2; ++t) {
+            sacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc += a[e] * bq[e];
+            for (int ks = 0; ks < 4; ++ks)
+                sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    as_frag(*reinterpret_cast<const uint4*>(k0 + (t * 4 + ks) * 512)), qf[ks], sacc[t], 0, 0, 0);
         }
-        return acc * scale;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int key = sl * 32 + 8 * lg + 4 * t + i;
+                sacc[t][i] = key <= qt ? sacc[t][i] * scale : -INFINITY;
+            }
     };
     float m = -INFINITY;
-    for (int c0 = 0; c0 <= t; c0 += 64) {
-        const int key = c0 + lane;
-        if (key <= t) m = fmaxf(m, score(key));
+    for (int sl = 0; sl < nsl; ++sl) {
+        f32x4 sacc[2];
+        scores(sl, sacc);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) m = fmaxf(m, sacc[t][i]);
     }
-    m = wave_max(m);
-    float l = 0.f, o0 = 0.f, o1 = 0.f;
-    for (int c0 = 0; c0 <= t; c0 += 64) {
-        const int key = c0 + lane;
-        const float p = (key <= t) ? __expf(score(key) - m) : 0.f;
-        l += p;
-        const float pb = round_bf(p);
-        const int nk = min(64, t + 1 - c0);
-        for (int j = 0; j < nk; ++j) {
-            const float pj = __shfl(pb, j, 64);
-            const uint32_t vv = *reinterpret_cast<const uint32_t*>(vb + (size_t)(c0 + j) * HD + 2 * lane);
-            o0 += pj * __uint_as_float(vv << 16);
-            o1 += pj * __uint_as_float(vv & 0xffff0000u);
-        }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+    f32x4 o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < nsl; ++sl) {
+        f32x4 sacc[2];
+        scores(sl, sacc);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float pv = __expf(sacc[t][i] - m);       // masked keys: exp(-inf) = 0
+                sacc[t][i] = pv;
+                l += pv;
+            }
+        const uint4 pa = make_uint4(pack2(sacc[0][0], sacc[0][1]), pack2(sacc[0][2], sacc[0][3]),
+                                    pack2(sacc[1][0], sacc[1][1]), pack2(sacc[1][2], sacc[1][3]));
+        const bf16_t* v0 = vb + (size_t)sl * 4096 + (lg * 16 + ln) * 8;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(*reinterpret_cast<const uint4*>(v0 + dt * 512)),
+                                                            as_frag(pa), o[dt], 0, 0, 0);
     }
-    l = wave_sum(l);
-    if (active) {
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    // o[dt][i] = O^T[dim = 16dt + 4lg + i][query q0 + ln]
+    if (q0 + ln < S) {
         const float inv = 1.0f / l;
-        *reinterpret_cast<uint32_t*>(out + ((size_t)(r * S + t) * H + h) * HD + 2 * lane) = pack2(o0 * inv, o1 * inv);
+        bf16_t* orow = out + ((size_t)(r * S + q0 + ln) * H + h) * HD;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            const int d = dt * 16 + lg * 4;
+            *reinterpret_cast<uint2*>(orow + d) =
+                make_uint2(pack2(o[dt][0] * inv, o[dt][1] * inv), pack2(o[dt][2] * inv, o[dt][3] * inv));
+        }
     }
 }
 
@@ -732,14 +767,15 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
     return 0;
 }
 
-extern "C" int zk_attn_prefill(const void* q, const void* k_cache, const void* v_rows, int R, int S, int H, int Hkv,
-                               int hd, int Smax, void* out, void* stream) {
+extern "C" int zk_attn_prefill(const void* q, const void* k_cache, const void* vt_cache, int R, int S, int H,
+                               int Hkv, int hd, int Smax, void* out, void* stream) {
     ZK_REQUIRE(hd == 128, "zk_attn_prefill: head_dim %d unsupported (128 only)", hd);
     ZK_REQUIRE(H % Hkv == 0, "zk_attn_prefill: H %% Hkv != 0");
     if (R * S == 0) return 0;
     const float scale = 1.0f / sqrtf((float)hd);
-    hipLaunchKernelGGL(k_attn_prefill, dim3((S + 3) / 4, H, R), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_rows, R, S, H, Hkv, Smax, scale,
+    ZK_REQUIRE(S <= Smax && Smax % 32 == 0, "zk_attn_prefill: S=%d Smax=%d", S, Smax);
+    hipLaunchKernelGGL(k_attn_prefill, dim3((S + 63) / 64, H, R), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)vt_cache, R, S, H, Hkv, Smax, scale,
                        (bf16_t*)out);
     ZK_CHECK_LAUNCH("zk_attn_prefill");
     return 0;

@@ -202,7 +202,12 @@ constexpr int WS_DA = ZK_WS_DA;  // activation chunks in flight (loader); WS_NB 
 constexpr int WS_THREADS = 320;
 constexpr int WS_PF = 4;         // weight chunks in flight per compute wave
 
-template <int MODE, int NCH, int PF>
+template <int N_>
+ZK_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
+
+// MT = 16-row M tiles actually present (1, 2, 4, 8): small batches stage and multiply only
+// the rows they have (B = 1 decode: 2 rows -> one 16-row tile instead of 8).
+template <int MODE, int NCH, int PF, int MT>
 __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
@@ -216,15 +221,16 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
     const int ln = lane & 15, lg = lane >> 4;
 
     if (w == 4) {
-        // ---------------- loader wave: 16 x 1 KB LDS-DMA pieces per 16 KB chunk
+        // ---------------- loader wave: 2*MT x 1 KB LDS-DMA pieces per chunk (16*MT rows x 64 k)
         // piece i covers tile rows 8i..8i+7; lane L lands at byte 16L of the piece:
         // row = 8i + (L>>3), slot = L&7  ->  source 16-B chunk = slot ^ (row&7)
+        constexpr int NP = 2 * MT;
         const int rl = lane >> 3, sl = lane & 7;
         auto issue = [&](int ch) {
-            char* dst = smem + (ch % WS_NB) * (BM * BK * 2);
+            char* dst = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
             const int k0 = kbeg + ch * BK;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < NP; ++i) {
                 const int row = 8 * i + rl;
                 const int m = min(row, M - 1);
                 const bf16_t* src = A + (size_t)m * lda + k0 + ((sl ^ (row & 7)) << 3);
@@ -239,10 +245,10 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         for (int c = 0; c < pre; ++c) issue(c);
         for (int c = 0; c < nchunks; ++c) {
             const int younger = min(c + WS_DA, nchunks) - c - 1;     // chunks issued after c
-            if (younger >= 3) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-            else if (younger == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-            else if (younger == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (younger >= 3) vm_wait<3 * NP>();
+            else if (younger == 2) vm_wait<2 * NP>();
+            else if (younger == 1) vm_wait<NP>();
+            else vm_wait<0>();
             __builtin_amdgcn_s_barrier();                           // publish chunk c
             asm volatile("" ::: "memory");
             if (c + WS_DA < nchunks) issue(c + WS_DA);              // its slot was read 2 chunks ago
@@ -254,9 +260,9 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
     const int wn = n0 + w * 16 + ln;
     const bool wvalid = wn < N;
     const bf16_t* wrow = w_base(W, n0 + w * 16, wvalid ? wn : 0, K, kbeg, lane);
-    f32x4 acc[8];
+    f32x4 acc[MT];
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     // Fully unrolled K loop (NCH chunks known at compile time): no loop back edge, so hipcc's
     // waitcnt pass counts exactly and keeps PF chunks (2 loads each) of weights in flight
     // (its loop-header merge otherwise drains the ring). Ring slots are compile-time indices.
@@ -276,12 +282,12 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         }
         __builtin_amdgcn_s_barrier();                               // chunk ch is in LDS
         asm volatile("" ::: "memory");
-        const char* base = smem + (ch % WS_NB) * (BM * BK * 2);
+        const char* base = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
+            for (int mt = 0; mt < MT; ++mt) {
 #ifndef ZK_DBG_NOMFMA
                 const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
                 acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
@@ -300,7 +306,7 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         float* C = Cpart + (size_t)split * M * N;
         if (wvalid) {
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt)
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int m = mt * 16 + lg * 4 + i;
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         const int F = N / 2;
         const int f = (n0 + w * 16) / 2 + (ln & 7);
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float mine = round_bf(acc[mt][i]);
@@ -371,15 +377,26 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     const int nchunks = K / nsplit / BK;
     if (M <= BM && nchunks <= 32) {
         dim3 g((N + BN - 1) / BN, 1, nsplit);
-        const size_t lds = (size_t)WS_NB * BM * BK * 2;
-#define ZK_WS_LAUNCH(MODE_, NCH_)                                                                                  \
+        const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
+        const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2;
+#define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
     do {                                                                                                          \
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, WS_PF>),                        \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                \
-        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, WS_PF>), g, dim3(WS_THREADS), lds, (hipStream_t)stream,        \
+        if (lds > 65536)                                                                                          \
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, WS_PF, MT_>),               \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
+        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, WS_PF, MT_>), g, dim3(WS_THREADS), lds, (hipStream_t)stream,   \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
                            skip_flag);                                                                             \
         handled = true;                                                                                           \
+    } while (0)
+#define ZK_WS_LAUNCH(MODE_, NCH_)                                                                                  \
+    do {                                                                                                          \
+        switch (MT) {                                                                                             \
+            case 1: ZK_WS_LAUNCH3(MODE_, NCH_, 1); break;                                                         \
+            case 2: ZK_WS_LAUNCH3(MODE_, NCH_, 2); break;                                                         \
+            case 4: ZK_WS_LAUNCH3(MODE_, NCH_, 4); break;                                                         \
+            default: ZK_WS_LAUNCH3(MODE_, NCH_, 8); break;                                                        \
+        }                                                                                                         \
     } while (0)
         bool handled = false;
         if (mode == 0) {
@@ -404,6 +421,7 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
             ZK_CHECK_LAUNCH("zk_gemm_bf16");
             return 0;
         }
+#undef ZK_WS_LAUNCH3
 #undef ZK_WS_LAUNCH
     }
     dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nsplit);

@@ -167,7 +167,6 @@ class HipDecoder:
             x=torch.empty(Mp, D, dtype=bf, device=dev), xn=torch.empty(Mp, D, dtype=bf, device=dev),
             q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
             h=torch.empty(Mp, Fd, dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
-            vrows=torch.empty(R * Hk * S_pre * hd, dtype=bf, device=dev),
             attn_work=torch.empty(max(1, R * Hk * attn_splits * (8 + 4 * hd)), dtype=f32, device=dev),
             scal=torch.zeros(16, dtype=i32, device=dev),
             eos_mode=torch.zeros(B, dtype=i32, device=dev), steps_after=torch.zeros(B, dtype=i32, device=dev),
@@ -210,8 +209,8 @@ class HipDecoder:
             call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
             if prefill:
                 call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
-                     ptr(kc), ptr(vt), ws["smax"], ptr(ws["vrows"]), self.rope_neox, skip, stream)
-                call("zk_attn_prefill", ptr(q), ptr(kc), ptr(ws["vrows"]), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
+                     ptr(kc), ptr(vt), ws["smax"], None, self.rope_neox, skip, stream)
+                call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
             elif self.fuse_qkv:
                 # in_proj epilogue fused into the attention launch (position = ctx - 1 = scal[1])
                 call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,

@@ -190,7 +190,6 @@ class HybridDecoder(HipDecoder):
             h=torch.empty(Mp, max(Fd, 1), dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
             yz=torch.empty(Mp, di, dtype=f32, device=dev), ym=torch.empty(Mp, di, dtype=bf, device=dev),
             xc=torch.empty(Mp, c.conv_dim, dtype=bf, device=dev),
-            vrows=torch.empty(R * Hk * S_pre * hd, dtype=bf, device=dev),
             attn_work=torch.empty(max(1, R * Hk * attn_splits * (8 + 4 * hd)), dtype=f32, device=dev),
             scal=torch.zeros(16, dtype=i32, device=dev),
             eos_mode=torch.zeros(B, dtype=i32, device=dev), steps_after=torch.zeros(B, dtype=i32, device=dev),
@@ -229,9 +228,8 @@ class HybridDecoder(HipDecoder):
                      stream)
                 if prefill:
                     call("zk_qkv_rope", ptr(part), 1, R, S, H, Hk, hd, ptr(self.freqs), 0, None, ptr(q), ptr(kc),
-                         ptr(vt), ws["smax"], ptr(ws["vrows"]), 1, skip, stream)
-                    call("zk_attn_prefill", ptr(q), ptr(kc), ptr(ws["vrows"]), R, S, H, Hk, hd, ws["smax"], ptr(y),
-                         stream)
+                         ptr(vt), ws["smax"], None, 1, skip, stream)
+                    call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
                 else:
                     call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
                          ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), 1, skip,
