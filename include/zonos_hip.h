@@ -249,6 +249,27 @@ int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* 
 int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias,
                    float* out, const int32_t* lens, int scale, void* stream);
 
+/* ---- DAC encoder (prefix audio -> codes; DACAutoencoder.encode, autoencoder.py:27-28 ->
+ * DacModel.encode). Convolutions run on zk_dac_conv_cl (channels-last fp16 operands); a strided
+ * Conv1d(k = 2s, stride s, pad ceil(s/2)) runs as a stride-1 3-tap conv over the input folded to
+ * [T/s][s*C] (weights repacked on the host). zk_dac_conv_cl accepts s_out = NULL (x_out only). */
+/* conv1 (1 -> C, k7, pad 3) of wav fp32 [B][T]: x_out fp32 [B][T][Cp], s_out = fp16(Snake(x)). */
+int zk_dac_enc_conv1(const float* wav, int B, int T, const float* w, const float* bias,
+                     const float* alpha_next, int C, int Cp, float* x_out, uint16_t* s_out, void* stream);
+/* Residual VQ encode of z fp32 [B][T][hidden] -> codes int64 [B][ncb][T]: per codebook
+ * e = normalize(in_w z + in_b); code = argmax_n -(|e|^2 - 2 e.cn_n) + |cn_n|^2 (first on ties,
+ * cn = normalised codebook); z -= out_w cb[code] + out_b (modeling_dac DacVectorQuantize). */
+int zk_dac_rvq_encode(const float* z, int B, int T, int hidden, int ncb, int ncode, int cdim,
+                      const float* in_w, const float* in_b, const float* cb_norm, const float* cb_norm_sq,
+                      const float* cb, const float* out_w, const float* out_b, int64_t* codes, void* stream);
+
+/* Resampler of DACAutoencoder.preprocess (autoencoder.py:21-25 -> torchaudio.functional.resample,
+ * sinc_interp_hann, lowpass_filter_width 6, rolloff 0.99): x fp32 [B][T] -> out fp32 [B][Tout],
+ * out[n] = sum_k kern[n % up][k] * x[(n / up) * down + k - width] (zero outside [0, T)), where
+ * up/down = new/orig rate over their gcd and kern [up][K = 2 width + down] the windowed-sinc table. */
+int zk_resample(const float* x, int B, long T, const float* kern, int up, int down, int width, int K,
+                float* out, long Tout, void* stream);
+
 /* ------------------------------------------------------------------ hybrid backbone: Mamba2 mixer
  * (zonos/backbone/_mamba_ssm.py -> mamba_ssm Mamba2; restated in oracle/hybrid_ref.py).
  * in_proj output columns [z (d_inner) | xBC (conv_dim = d_inner + 2 d_state) | dt (nheads)].

@@ -29,6 +29,8 @@ class DacCfg:
     codebook_size: int = 1024
     codebook_dim: int = 8
     sampling_rate: int = 44100
+    encoder_hidden_size: int = 64
+    downsampling_ratios: tuple = (2, 4, 8, 8)
 
     @property
     def hop_length(self):
@@ -153,3 +155,98 @@ def decode_list(W, c: DacCfg, codes_list) -> list:
             continue
         out.append(decode(W, c, x).squeeze(0))
     return out
+
+
+# ----------------------------------------------------------------------------------------
+# Encoder (prefix audio -> codes): DACAutoencoder.encode (autoencoder.py:27-28) ->
+# DacModel.encode -> DacEncoder (modeling_dac.py DacEncoder / DacEncoderBlock / DacResidualUnit)
+# -> DacResidualVectorQuantizer / DacVectorQuantize.decode_latents (cosine nearest code).
+# ----------------------------------------------------------------------------------------
+
+def enc_weight_shapes(c: DacCfg) -> dict:
+    s = {}
+    e = c.encoder_hidden_size
+    s["encoder.conv1.weight"] = (e, 1, 7)
+    s["encoder.conv1.bias"] = (e,)
+    for i, st in enumerate(c.downsampling_ratios):
+        dim = e * 2 ** (i + 1)
+        b = f"encoder.block.{i}."
+        for r in (1, 2, 3):
+            u = b + f"res_unit{r}."
+            s[u + "snake1.alpha"] = (1, dim // 2, 1)
+            s[u + "conv1.weight"] = (dim // 2, dim // 2, 7)
+            s[u + "conv1.bias"] = (dim // 2,)
+            s[u + "snake2.alpha"] = (1, dim // 2, 1)
+            s[u + "conv2.weight"] = (dim // 2, dim // 2, 1)
+            s[u + "conv2.bias"] = (dim // 2,)
+        s[b + "snake1.alpha"] = (1, dim // 2, 1)
+        s[b + "conv1.weight"] = (dim, dim // 2, 2 * st)
+        s[b + "conv1.bias"] = (dim,)
+    d = e * 2 ** len(c.downsampling_ratios)
+    s["encoder.snake1.alpha"] = (1, d, 1)
+    s["encoder.conv2.weight"] = (c.hidden_size, d, 3)
+    s["encoder.conv2.bias"] = (c.hidden_size,)
+    for k in range(c.n_codebooks):
+        q = f"quantizer.quantizers.{k}."
+        s[q + "in_proj.weight"] = (c.codebook_dim, c.hidden_size, 1)
+        s[q + "in_proj.bias"] = (c.codebook_dim,)
+    return s
+
+
+def make_enc_weights(c: DacCfg = DAC_44KHZ, seed: int = 0, gain: float = 0.5) -> dict:
+    """Seeded encoder + quantizer-encode weights (the decode-side quantizer weights come from
+    make_dac_weights with the same seed)."""
+    out = {}
+    for idx, (k, shape) in enumerate(enc_weight_shapes(c).items()):
+        g = torch.Generator().manual_seed(seed * 1_000_003 + 7919 * idx + 99991)
+        if k.endswith("alpha"):
+            t = 0.5 + torch.rand(shape, generator=g)
+        elif k.endswith("bias"):
+            t = 0.05 * torch.randn(shape, generator=g)
+        else:
+            fan_in = shape[1] * shape[2]
+            t = torch.randn(shape, generator=g) * (gain / math.sqrt(fan_in))
+        out[k] = t.float()
+    return out
+
+
+def encoder(W, c: DacCfg, wav: torch.Tensor) -> torch.Tensor:
+    """DacEncoder.forward: wav [B,1,T] -> latent [B, hidden, T/hop]."""
+    x = F.conv1d(wav, W["encoder.conv1.weight"], W["encoder.conv1.bias"], padding=3)
+    for i, st in enumerate(c.downsampling_ratios):
+        b = f"encoder.block.{i}."
+        for r, dil in ((1, 1), (2, 3), (3, 9)):
+            x = res_unit(W, b + f"res_unit{r}.", x, dil)
+        x = F.conv1d(snake(x, W[b + "snake1.alpha"]), W[b + "conv1.weight"], W[b + "conv1.bias"], stride=st,
+                     padding=math.ceil(st / 2))
+    return F.conv1d(snake(x, W["encoder.snake1.alpha"]), W["encoder.conv2.weight"], W["encoder.conv2.bias"],
+                    padding=1)
+
+
+def quantize(W, c: DacCfg, z: torch.Tensor, margins: list | None = None) -> torch.Tensor:
+    """DacResidualVectorQuantizer.forward (eval): per codebook in_proj -> L2-normalised nearest
+    code (max of -(|e|^2 - 2 e.c) + |c|^2) -> codebook row -> out_proj -> residual update.
+    ``margins`` (optional) receives per codebook the top-1/top-2 distance gap [B, T]."""
+    B, _, T = z.shape
+    residual = z
+    codes = []
+    for k in range(c.n_codebooks):
+        q = f"quantizer.quantizers.{k}."
+        proj = F.conv1d(residual, W[q + "in_proj.weight"], W[q + "in_proj.bias"])
+        enc = F.normalize(proj.permute(0, 2, 1).reshape(B * T, -1))
+        cb = F.normalize(W[q + "codebook.weight"])
+        dist = -(enc.pow(2).sum(1, keepdim=True) - 2 * enc @ cb.t()) + cb.pow(2).sum(1, keepdim=True).t()
+        idx = dist.max(1)[1]
+        if margins is not None:
+            top = dist.topk(2, dim=1).values
+            margins.append((top[:, 0] - top[:, 1]).reshape(B, T))
+        idx = idx.reshape(B, T)
+        quant = F.embedding(idx, W[q + "codebook.weight"]).transpose(1, 2)
+        residual = residual - F.conv1d(quant, W[q + "out_proj.weight"], W[q + "out_proj.bias"])
+        codes.append(idx)
+    return torch.stack(codes, dim=1)
+
+
+def encode(W, c: DacCfg, wav: torch.Tensor, margins: list | None = None):
+    z = encoder(W, c, wav)
+    return z, quantize(W, c, z, margins)

@@ -23,6 +23,7 @@ oracle.dac_ref.make_dac_weights, and a checksum of them is stored for verificati
 from __future__ import annotations
 
 import hashlib
+import math
 import os
 import sys
 import types
@@ -306,9 +307,51 @@ def make_dac_fixtures():
                             cfg=np.array([c.hidden_size, c.decoder_hidden_size, *c.upsampling_ratios]))
 
 
+ENC_DAC = dac_ref.DacCfg(hidden_size=64, decoder_hidden_size=64, upsampling_ratios=(8, 8, 4, 2),
+                         encoder_hidden_size=32, downsampling_ratios=(2, 4, 8, 8))
+
+
+def make_dac_encoder_fixture():
+    """DacModel.encode (the reference's DACAutoencoder.encode, autoencoder.py:27-28) on a reduced-width
+    encoder with the 44.1 kHz strides (2, 4, 8, 8): input waveform, latent and codes."""
+    c, seed = ENC_DAC, 5
+    W = dict(dac_ref.make_dac_weights(c, seed=seed))
+    W.update(dac_ref.make_enc_weights(c, seed=seed))
+    hf = DacModel(DacConfig(sampling_rate=44100, hidden_size=c.hidden_size, decoder_hidden_size=c.decoder_hidden_size,
+                            upsampling_ratios=list(c.upsampling_ratios), encoder_hidden_size=c.encoder_hidden_size,
+                            downsampling_ratios=list(c.downsampling_ratios), n_codebooks=c.n_codebooks,
+                            codebook_size=c.codebook_size, codebook_dim=c.codebook_dim))
+    sd = hf.state_dict()
+    for k, v in W.items():
+        assert sd[k].shape == v.shape, (k, sd[k].shape, v.shape)
+        sd[k] = v
+    missing = [k for k in sd if k.startswith(("encoder.", "quantizer.")) and k not in W]
+    assert not missing, missing[:5]
+    hf.load_state_dict(sd)
+    hf.eval()
+    g = torch.Generator().manual_seed(seed + 7)
+    T = 512 * 24
+    t = torch.arange(T) / 44100.0
+    wav = (0.3 * torch.sin(2 * math.pi * 180 * t) * torch.sin(2 * math.pi * 2.5 * t)).expand(2, 1, T).clone()
+    wav += 0.05 * torch.randn(2, 1, T, generator=g)
+    with torch.no_grad():
+        z_ref = hf.encoder(wav)
+        codes = hf.encode(wav).audio_codes
+        z_o, codes_o = dac_ref.encode(W, c, wav)
+    print(f"[dac_enc] latent max|d| {(z_o - z_ref).abs().max().item():.2e}, codes equal "
+          f"{torch.equal(codes_o, codes)}")
+    assert (z_o - z_ref).abs().max().item() < 1e-4 and torch.equal(codes_o, codes)
+    np.savez_compressed(os.path.join(HERE, "dac_enc.npz"), wav=wav.numpy(), z=z_ref.numpy(),
+                        codes=codes.numpy().astype(np.int16), seed=np.int64(seed))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
+    if len(sys.argv) > 1 and sys.argv[1] == "enc":
+        make_dac_encoder_fixture()
+        sys.exit(0)
     make_delay_fixtures()
     make_sampler_fixtures()
     make_generate_fixtures()
     make_dac_fixtures()
+    make_dac_encoder_fixture()

@@ -10,6 +10,19 @@ from oracle import dac_ref, zonos_ref
 G = os.path.join(os.path.dirname(__file__), "golden")
 TINY = zonos_ref.BackboneCfg(d_model=256, n_layer=2, n_heads=2, n_kv=1, d_ff=512)
 TINY_DAC = dac_ref.DacCfg(hidden_size=64, decoder_hidden_size=64, upsampling_ratios=(4, 2))
+ENC_DAC = dac_ref.DacCfg(hidden_size=64, decoder_hidden_size=64, upsampling_ratios=(8, 8, 4, 2),
+                         encoder_hidden_size=32, downsampling_ratios=(2, 4, 8, 8))
+
+
+def load_enc_case():
+    """dac_enc.npz (DacModel.encode on ENC_DAC) + the oracle weights that produced it."""
+    d = np.load(os.path.join(G, "dac_enc.npz"))
+    seed = int(d["seed"])
+    W = dict(dac_ref.make_dac_weights(ENC_DAC, seed=seed))
+    W.update(dac_ref.make_enc_weights(ENC_DAC, seed=seed))
+    return W, torch.from_numpy(d["wav"]), torch.from_numpy(d["z"]), torch.from_numpy(d["codes"].astype(np.int64))
+
+
 GEN_CASES = ["greedy", "greedy_rep", "sampled_cli", "sampled_knobs", "eos_greedy", "eos_sampled"]
 
 

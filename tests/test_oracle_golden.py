@@ -10,7 +10,7 @@ import torch
 from oracle import dac_ref, zonos_ref
 from oracle.philox import exp_noise, philox4x32_10
 
-from .golden_util import GEN_CASES, TINY, TINY_DAC, load_gen_case, wsum
+from .golden_util import ENC_DAC, GEN_CASES, TINY, TINY_DAC, load_enc_case, load_gen_case, wsum
 
 G = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -83,3 +83,12 @@ def test_dac_golden(name):
     L = int(d["short_len"])
     got_s = dac_ref.decode_list(W, c, [codes[1, :, :L]])[0]
     assert (got_s - torch.from_numpy(d["wav_short"][0])).abs().max().item() < 1e-5
+
+
+def test_dac_encoder_golden():
+    """oracle DAC encoder + RVQ encode == transformers DacModel.encode (dac_enc.npz)."""
+    W, wav, z_ref, codes_ref = load_enc_case()
+    with torch.no_grad():
+        z, codes = dac_ref.encode(W, ENC_DAC, wav)
+    assert (z - z_ref).abs().max().item() < 1e-4
+    assert torch.equal(codes, codes_ref)

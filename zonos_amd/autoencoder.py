@@ -330,8 +330,149 @@ class HipDacDecoder:
         return [r for r in results if r is not None]
 
 
+class HipDacEncoder:
+    """DAC encoder + residual-VQ encode on the GPU: DACAutoencoder.encode (autoencoder.py:27-28)
+    -> DacModel.encode (modeling_dac DacEncoder, DacResidualVectorQuantizer eval path).
+
+    Channels-last, on the same conv kernel as the decoder (zk_dac_conv_cl: fp16 operands, fp32
+    accumulation, fp32 residual stream -- the reference runs this fp32 under cuDNN's default
+    TF32 convolutions, a comparable 10-bit-mantissa operand precision). The strided
+    Conv1d(k=2s, stride s, pad s/2) of each block runs as a stride-1 3-tap convolution over the
+    activation viewed as [T/s][s*C] (a free reshape of channels-last memory) with host-repacked
+    weights W'[tap][co][j*C+ci] = W[co][ci][(tap-1)s + j + s/2]."""
+
+    def __init__(self, spec: "DacSpec", state_dict: dict, device="cuda"):
+        _lib.load()
+        self.spec = spec
+        self.device = dev = torch.device(device)
+        sd = _fold_weight_norm(state_dict)
+        P = HipDacDecoder._pad32
+        stream = _lib.stream_ptr(dev)
+
+        def t(k):
+            return sd[k].to(device=dev, dtype=torch.float32).contiguous()
+
+        def w16(w):                          # fp32 [Cout][Cin][ks] (padded) -> fp16 [ks][Cout][Cin]
+            co, ci, ks = w.shape
+            out = torch.empty(ks * co * ci, dtype=torch.int16, device=dev)
+            call("zk_dac_prep_w16", ptr(w.contiguous()), co, ci, ks, 1, 0, ptr(out), None, stream)
+            return out
+
+        def wconv(w):
+            co, ci, ks = w.shape
+            wp = torch.zeros(P(co), P(ci), ks, device=dev)
+            wp[:co, :ci] = w
+            return w16(wp)
+
+        def wstrided(w, st):                 # [Cout][Cin][2s] -> folded 3-tap [Cout_p][s*Cin_p][3]
+            co, ci, k2 = w.shape
+            assert k2 == 2 * st and st % 2 == 0, "strided encoder conv: k = 2*stride, even stride"
+            cip = P(ci)
+            wf = torch.zeros(P(co), st, cip, 3, device=dev)
+            for tap in range(3):
+                for j in range(st):
+                    k = (tap - 1) * st + j + st // 2
+                    if 0 <= k < k2:
+                        wf[:co, j, :ci, tap] = w[:, :, k]
+            return w16(wf.reshape(P(co), st * cip, 3))
+
+        def vec(v, fill):
+            out = torch.full((P(v.numel()),), fill, device=dev)
+            out[:v.numel()] = v.reshape(-1)
+            return out
+
+        w1 = t("encoder.conv1.weight")
+        self.c0 = w1.shape[0]
+        self.conv1_w, self.conv1_b = w1.reshape(self.c0, 7), t("encoder.conv1.bias")
+        self.blocks = []
+        i = 0
+        while f"encoder.block.{i}.conv1.weight" in sd:
+            p = f"encoder.block.{i}."
+            wb = t(p + "conv1.weight")
+            st = wb.shape[2] // 2
+            blk = {"stride": st, "cin": P(wb.shape[1]), "cout": P(wb.shape[0]), "alpha": vec(t(p + "snake1.alpha"), 1.0),
+                   "w": wstrided(wb, st), "b": vec(t(p + "conv1.bias"), 0.0), "res": []}
+            for r, dil in ((1, 1), (2, 3), (3, 9)):
+                u = p + f"res_unit{r}."
+                blk["res"].append({"dil": dil, "a1": vec(t(u + "snake1.alpha"), 1.0), "w1": wconv(t(u + "conv1.weight")),
+                                   "b1": vec(t(u + "conv1.bias"), 0.0), "a2": vec(t(u + "snake2.alpha"), 1.0),
+                                   "w2": wconv(t(u + "conv2.weight")), "b2": vec(t(u + "conv2.bias"), 0.0)})
+            self.blocks.append(blk)
+            i += 1
+        self.final_alpha = vec(t("encoder.snake1.alpha"), 1.0)
+        w2 = t("encoder.conv2.weight")
+        self.hidden = w2.shape[0]
+        self.conv2_w, self.conv2_b = wconv(w2), vec(t("encoder.conv2.bias"), 0.0)
+        self.cd = spec.codebook_dim
+        K = spec.n_codebooks
+        q = "quantizer.quantizers.{}."
+        self.in_w = torch.stack([t(q.format(k) + "in_proj.weight").reshape(self.cd, self.hidden) for k in range(K)])
+        self.in_b = torch.stack([t(q.format(k) + "in_proj.bias") for k in range(K)])
+        self.cb = torch.stack([t(q.format(k) + "codebook.weight") for k in range(K)])
+        self.cbn = torch.nn.functional.normalize(self.cb, dim=2).contiguous()   # one-time weight prep
+        self.cbn2 = self.cbn.pow(2).sum(2).contiguous()
+        self.out_w = torch.stack([t(q.format(k) + "out_proj.weight").reshape(self.hidden, self.cd) for k in range(K)])
+        self.out_b = torch.stack([t(q.format(k) + "out_proj.bias") for k in range(K)])
+        self.hop = int(math.prod(b["stride"] for b in self.blocks))
+        torch.cuda.synchronize(dev)
+
+    def latents(self, wav: torch.Tensor) -> torch.Tensor:
+        """DacEncoder.forward: wav [B, 1, T] (T a multiple of the hop) -> z fp32 [B, T/hop, hidden]."""
+        assert wav.dim() == 3 and wav.shape[1] == 1, "expected [B, 1, T]"
+        B, _, T = wav.shape
+        assert T % self.hop == 0, f"T={T} must be a multiple of the hop {self.hop} (see preprocess)"
+        dev, P, f16 = self.device, HipDacDecoder._pad32, torch.int16
+        stream = _lib.stream_ptr(dev)
+        wav = wav.to(dev, torch.float32).contiguous()
+        C = P(self.c0)
+        first_alpha = self.blocks[0]["res"][0]["a1"] if self.blocks else self.final_alpha
+        x = torch.empty(B, T, C, device=dev)
+        act = torch.empty(B, T, C, dtype=f16, device=dev)
+        call("zk_dac_enc_conv1", ptr(wav), B, T, ptr(self.conv1_w), ptr(self.conv1_b), ptr(first_alpha), self.c0, C,
+             ptr(x), ptr(act), stream)
+        L = T
+        for bi, blk in enumerate(self.blocks):
+            C = blk["cin"]
+            tmp = torch.empty_like(act)
+            for j, ru in enumerate(blk["res"]):
+                d = ru["dil"]
+                a_next = blk["res"][j + 1]["a1"] if j + 1 < len(blk["res"]) else blk["alpha"]
+                call("zk_dac_conv_cl", ptr(act), B, C, L, ptr(ru["w1"]), 0, ptr(ru["b1"]), C, 7, d, 3 * d, L,
+                     1, 1, 0, L, None, None, ptr(ru["a2"]), ptr(tmp), 0, None, 1, 1, stream)
+                call("zk_dac_conv_cl", ptr(tmp), B, C, L, ptr(ru["w2"]), 0, ptr(ru["b2"]), C, 1, 1, 0, L,
+                     1, 1, 0, L, ptr(x), ptr(x), ptr(a_next), ptr(act), 0, None, 1, 1, stream)
+            del tmp
+            st, Co = blk["stride"], blk["cout"]
+            Lo = L // st
+            a_next = self.blocks[bi + 1]["res"][0]["a1"] if bi + 1 < len(self.blocks) else self.final_alpha
+            x = torch.empty(B, Lo, Co, device=dev)
+            s_new = torch.empty(B, Lo, Co, dtype=f16, device=dev)
+            call("zk_dac_conv_cl", ptr(act), B, st * C, Lo, ptr(blk["w"]), 0, ptr(blk["b"]), Co, 3, 1, 1, Lo,
+                 1, 1, 0, Lo, None, ptr(x), ptr(a_next), ptr(s_new), 0, None, 1, 1, stream)
+            act, L = s_new, Lo
+        Hp = P(self.hidden)
+        z = torch.empty(B, L, Hp, device=dev)
+        call("zk_dac_conv_cl", ptr(act), B, act.shape[2], L, ptr(self.conv2_w), 0, ptr(self.conv2_b), Hp, 3, 1, 1, L,
+             1, 1, 0, L, None, ptr(z), None, None, 0, None, 1, 1, stream)
+        return z[:, :, :self.hidden] if Hp != self.hidden else z
+
+    def quantize(self, z: torch.Tensor) -> torch.Tensor:
+        """DacResidualVectorQuantizer (eval, all codebooks): z fp32 [B, T, hidden] -> int64 [B, K, T]."""
+        z = z.contiguous()
+        B, T, H = z.shape
+        K = self.in_w.shape[0]
+        codes = torch.empty(B, K, T, dtype=torch.int64, device=self.device)
+        call("zk_dac_rvq_encode", ptr(z), B, T, H, K, self.cb.shape[1], self.cd, ptr(self.in_w), ptr(self.in_b),
+             ptr(self.cbn), ptr(self.cbn2), ptr(self.cb), ptr(self.out_w), ptr(self.out_b), ptr(codes),
+             _lib.stream_ptr(self.device))
+        return codes
+
+    def encode(self, wav: torch.Tensor) -> torch.Tensor:
+        return self.quantize(self.latents(wav))
+
+
 class DACAutoencoder:
-    """API mirror of zonos/autoencoder.py:12-268 (decode side).
+    """API mirror of zonos/autoencoder.py:12-268 (prefix encode + decode + post-processing).
 
     Weights: ``DACAutoencoder(state_dict=...)``, ``DACAutoencoder.from_local(dir_or_file)``
     (a HF-format DacModel safetensors), or the local HF cache of "descript/dac_44khz"
@@ -344,6 +485,8 @@ class DACAutoencoder:
             if cfg is not None:
                 self.spec = DacSpec.from_hf_config(cfg)
         self.decoder = HipDacDecoder(self.spec, state_dict, device)
+        self._encoder = None
+        self._state_dict = state_dict if any(k.startswith("encoder.") for k in state_dict) else None
         self.codebook_size = self.spec.codebook_size
         self.num_codebooks = self.spec.n_codebooks
         self.sampling_rate = self.spec.sampling_rate
@@ -352,6 +495,36 @@ class DACAutoencoder:
     def from_local(cls, path: str, device="cuda") -> "DACAutoencoder":
         sd, cfg = _load_safetensors_dir(path)
         return cls(sd, DacSpec.from_hf_config(cfg) if cfg else None, device)
+
+    # ---- prefix-audio side (autoencoder.py:21-42)
+    @property
+    def encoder(self) -> HipDacEncoder:
+        if self._encoder is None:
+            if self._state_dict is None:
+                raise ValueError("the DAC state dict has no encoder.* weights; encode() needs the full DacModel")
+            self._encoder = HipDacEncoder(self.spec, self._state_dict, self.decoder.device)
+            self._state_dict = None
+        return self._encoder
+
+    def preprocess(self, wav: torch.Tensor, sr: int) -> torch.Tensor:
+        """autoencoder.py:21-25: resample to 44.1 kHz (windowed-sinc, on the GPU), left-pad to a
+        multiple of 512 samples."""
+        from . import audio
+        wav = audio.resample(wav.to(self.decoder.device, torch.float32), sr, self.sampling_rate)
+        return audio.left_pad(wav, 512)
+
+    def encode(self, wav: torch.Tensor) -> torch.Tensor:
+        """autoencoder.py:27-28 (DacModel.encode(wav).audio_codes): [B, 1, T] -> int64 [B, 9, T/512]."""
+        return self.encoder.encode(wav)
+
+    def load_prefix_audio(self, audio_path: str, device=None) -> torch.Tensor:
+        """autoencoder.py:30-42: read, average channels to mono, preprocess, encode -> [1, 9, T]."""
+        from . import audio
+        wav, sr = audio.read_wav(audio_path)
+        wav = wav.mean(dim=0, keepdim=True)
+        wav = self.preprocess(wav, sr)
+        codes = self.encode(wav.unsqueeze(0))
+        return codes if device is None else codes.to(device)
 
     def decode(self, codes: torch.Tensor) -> torch.Tensor:
         """autoencoder.py:44-47: [B, 9, T] -> fp32 [B, 1, 512*T] (all rows full length)."""

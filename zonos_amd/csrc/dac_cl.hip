@@ -209,7 +209,7 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
     for (int m = 0; m < FM; ++m) {
         const int co = co0 + wm * 16 * FM + m * 16 + lg * 4;
         const float4 bb = *reinterpret_cast<const float4*>(bias + co);
-        const float4 aa = *reinterpret_cast<const float4*>(alpha + co);
+        const float4 aa = sout ? *reinterpret_cast<const float4*>(alpha + co) : make_float4(1.f, 1.f, 1.f, 1.f);
         const float r0 = __fdiv_rn(1.0f, __fadd_rn(aa.x, 1e-9f)), r1 = __fdiv_rn(1.0f, __fadd_rn(aa.y, 1e-9f));
         const float r2 = __fdiv_rn(1.0f, __fadd_rn(aa.z, 1e-9f)), r3 = __fdiv_rn(1.0f, __fadd_rn(aa.w, 1e-9f));
 #pragma unroll
@@ -233,6 +233,7 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
                 }
             }
             if (xout) *reinterpret_cast<float4*>(xout + o) = make_float4(v0, v1, v2, v3);
+            if (!sout) continue;
             if (s_f32)      // fp32 Snake output for the fp32 tail (exact sinf, reference formula)
                 reinterpret_cast<float4*>(sout)[o >> 2] =
                     make_float4(snake(v0, aa.x), snake(v1, aa.y), snake(v2, aa.z), snake(v3, aa.w));
@@ -299,6 +300,124 @@ __global__ __launch_bounds__(256) void k_tail_cl(const float* __restrict__ s, in
     out[(size_t)b * T + t] = (t < len) ? tanhf(__fadd_rn(acc, bias[0])) : 0.f;
 }
 
+// ---------------------------------------------------------------- encoder (prefix audio)
+// DacEncoder.conv1 (1 -> C channels, k7, pad 3) from the waveform, channels-last outputs: fp32
+// x (residual stream of the first residual unit) and fp16 Snake_a(x) (its conv input).
+__global__ __launch_bounds__(256) void k_enc_conv1(const float* __restrict__ wav, int T, const float* __restrict__ w,
+                                                   const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                   int C, int Cp, float* __restrict__ x, uint16_t* __restrict__ s) {
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (idx >= (long)T * Cp) return;
+    const int c = (int)(idx % Cp);
+    const int t = (int)(idx / Cp);
+    float v = 0.f, sv = 0.f;
+    if (c < C) {
+        const float* wb = wav + (size_t)b * T;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const int u = t + k - 3;
+            acc += w[c * 7 + k] * ((u >= 0 && u < T) ? wb[u] : 0.f);
+        }
+        v = acc + bias[c];
+        sv = snake_fast(v, alpha[c], __fdiv_rn(1.0f, __fadd_rn(alpha[c], 1e-9f)));
+    }
+    const size_t o = ((size_t)b * T + t) * Cp + c;
+    x[o] = v;
+    s[o] = __builtin_bit_cast(uint16_t, (_Float16)sv);
+}
+
+// DacResidualVectorQuantizer (eval) for one latent frame per workgroup: per codebook in_proj
+// (hidden -> cd), L2 normalisation, nearest normalised code by the reference's distance
+// -(|e|^2 - 2 e.c) + |c|^2 (first index of the max), codebook row -> out_proj -> residual update.
+constexpr int RVQ_CD = 8;
+__global__ __launch_bounds__(256) void k_rvq_encode(const float* __restrict__ z, int T, int hidden, int ncb, int ncode,
+                                                    const float* __restrict__ in_w, const float* __restrict__ in_b,
+                                                    const float* __restrict__ cbn, const float* __restrict__ cbn2,
+                                                    const float* __restrict__ cb, const float* __restrict__ out_w,
+                                                    const float* __restrict__ out_b, int64_t* __restrict__ codes) {
+    extern __shared__ float sm[];                       // residual [hidden]
+    __shared__ float red[4][RVQ_CD];
+    __shared__ float bestv[4];
+    __shared__ int besti[4];
+    __shared__ float qv[RVQ_CD];
+    const int t = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const float* zr = z + ((size_t)b * T + t) * hidden;
+    for (int c = tid; c < hidden; c += 256) sm[c] = zr[c];
+    __syncthreads();
+    for (int k = 0; k < ncb; ++k) {
+        // in_proj
+        float part[RVQ_CD];
+#pragma unroll
+        for (int j = 0; j < RVQ_CD; ++j) part[j] = 0.f;
+        const float* wk = in_w + (size_t)k * RVQ_CD * hidden;
+        for (int c = tid; c < hidden; c += 256) {
+            const float r = sm[c];
+#pragma unroll
+            for (int j = 0; j < RVQ_CD; ++j) part[j] += wk[(size_t)j * hidden + c] * r;
+        }
+#pragma unroll
+        for (int j = 0; j < RVQ_CD; ++j) {
+            float v = part[j];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (lane == 0) red[wv][j] = v;
+        }
+        __syncthreads();
+        float e[RVQ_CD];
+        float nrm = 0.f;
+#pragma unroll
+        for (int j = 0; j < RVQ_CD; ++j) {
+            e[j] = red[0][j] + red[1][j] + red[2][j] + red[3][j] + in_b[k * RVQ_CD + j];
+            nrm += e[j] * e[j];
+        }
+        const float inv = 1.0f / fmaxf(sqrtf(nrm), 1e-12f);
+        float l2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < RVQ_CD; ++j) {
+            e[j] *= inv;
+            l2 += e[j] * e[j];
+        }
+        // nearest code
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        const float* cbk = cbn + (size_t)k * ncode * RVQ_CD;
+        for (int n = tid; n < ncode; n += 256) {
+            float dot = 0.f;
+#pragma unroll
+            for (int j = 0; j < RVQ_CD; ++j) dot += e[j] * cbk[n * RVQ_CD + j];
+            const float d = -(l2 - 2.0f * dot) + cbn2[k * ncode + n];
+            if (d > bv || (d == bv && n < bi)) { bv = d; bi = n; }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const float ov = __shfl_xor(bv, off, 64);
+            const int oi = __shfl_xor(bi, off, 64);
+            if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        if (lane == 0) { bestv[wv] = bv; besti[wv] = bi; }
+        __syncthreads();
+        if (tid == 0) {
+            float v = bestv[0];
+            int i = besti[0];
+            for (int w2 = 1; w2 < 4; ++w2)
+                if (bestv[w2] > v || (bestv[w2] == v && besti[w2] < i)) { v = bestv[w2]; i = besti[w2]; }
+            codes[((size_t)b * ncb + k) * T + t] = i;
+#pragma unroll
+            for (int j = 0; j < RVQ_CD; ++j) qv[j] = cb[((size_t)k * ncode + i) * RVQ_CD + j];
+        }
+        __syncthreads();
+        const float* ow = out_w + (size_t)k * hidden * RVQ_CD;
+        for (int c = tid; c < hidden; c += 256) {
+            float acc = 0.f;
+#pragma unroll
+            for (int j = 0; j < RVQ_CD; ++j) acc += ow[(size_t)c * RVQ_CD + j] * qv[j];
+            sm[c] -= acc + out_b[(size_t)k * hidden + c];
+        }
+        __syncthreads();
+    }
+}
+
 template <int FM>
 void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Cin, int Tin, const uint16_t* w,
                  long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
@@ -313,6 +432,30 @@ void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Ci
 }
 
 }  // namespace
+
+extern "C" int zk_dac_enc_conv1(const float* wav, int B, int T, const float* w, const float* bias,
+                                const float* alpha_next, int C, int Cp, float* x_out, uint16_t* s_out, void* stream) {
+    ZK_REQUIRE(C > 0 && Cp >= C && Cp % 32 == 0, "zk_dac_enc_conv1: C=%d Cp=%d", C, Cp);
+    if (B == 0 || T == 0) return 0;
+    const long n = (long)T * Cp;
+    hipLaunchKernelGGL(k_enc_conv1, dim3((unsigned)((n + 255) / 256), B), dim3(256), 0, (hipStream_t)stream, wav, T, w,
+                       bias, alpha_next, C, Cp, x_out, s_out);
+    ZK_CHECK_LAUNCH("zk_dac_enc_conv1");
+    return 0;
+}
+
+extern "C" int zk_dac_rvq_encode(const float* z, int B, int T, int hidden, int ncb, int ncode, int cdim,
+                                 const float* in_w, const float* in_b, const float* cb_norm, const float* cb_norm_sq,
+                                 const float* cb, const float* out_w, const float* out_b, int64_t* codes,
+                                 void* stream) {
+    ZK_REQUIRE(cdim == RVQ_CD && hidden > 0 && ncb > 0 && ncode > 0, "zk_dac_rvq_encode: cdim=%d (8 only)", cdim);
+    ZK_REQUIRE((size_t)hidden * 4 <= 64 * 1024, "zk_dac_rvq_encode: hidden=%d too large", hidden);
+    if (B == 0 || T == 0) return 0;
+    hipLaunchKernelGGL(k_rvq_encode, dim3(T, B), dim3(256), (size_t)hidden * 4, (hipStream_t)stream, z, T, hidden, ncb,
+                       ncode, in_w, in_b, cb_norm, cb_norm_sq, cb, out_w, out_b, codes);
+    ZK_CHECK_LAUNCH("zk_dac_rvq_encode");
+    return 0;
+}
 
 extern "C" int zk_dac_rvq_decode_cl(const int64_t* codes, int B, int ncb, int T, long code_bstride,
                                     const float* tables, int ncode, int hidden, int cpad, uint16_t* z,
@@ -334,7 +477,8 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     ZK_REQUIRE(Cin > 0 && Cin % 32 == 0, "zk_dac_conv_cl: Cin=%d must be a multiple of 32", Cin);
     ZK_REQUIRE(Cout > 0 && Cout % 32 == 0, "zk_dac_conv_cl: Cout=%d must be a multiple of 32", Cout);
     ZK_REQUIRE(ks >= 1 && ks <= 7 && dil >= 1 && (ks - 1) * dil <= MAXSPAN, "zk_dac_conv_cl: ks=%d dil=%d", ks, dil);
-    ZK_REQUIRE(nphase >= 1 && alpha_next != nullptr && s_out != nullptr && bias != nullptr,
+    ZK_REQUIRE(nphase >= 1 && bias != nullptr && (s_out == nullptr || alpha_next != nullptr) &&
+                   (s_out != nullptr || x_out != nullptr),
                "zk_dac_conv_cl: bad arguments");
     if (B == 0 || Qn <= 0) return 0;
     const int nco = Cout / 32;

@@ -145,7 +145,37 @@ __global__ __launch_bounds__(64) void k_gate(const double* __restrict__ z, int B
     }
 }
 
+// Polyphase windowed-sinc resampler (DACAutoencoder.preprocess -> torchaudio.functional.resample,
+// autoencoder.py:21-25): out[n] = sum_k kern[n % up][k] * x[(n / up) * down + k - width], zero
+// outside [0, T); fp32 taps in order k = 0..K-1. One thread per output sample.
+__global__ __launch_bounds__(256) void k_resample(const float* __restrict__ x, long T, const float* __restrict__ kern,
+                                                  int up, int down, int width, int K, float* __restrict__ out,
+                                                  long Tout) {
+    const long n = (long)blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (n >= Tout) return;
+    const float* xb = x + (size_t)b * T;
+    const float* kp = kern + (size_t)(n % up) * K;
+    const long base = (n / up) * down - width;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) {
+        const long u = base + k;
+        if (u >= 0 && u < T) acc = __fadd_rn(acc, __fmul_rn(kp[k], xb[u]));
+    }
+    out[(size_t)b * Tout + n] = acc;
+}
+
 }  // namespace
+
+extern "C" int zk_resample(const float* x, int B, long T, const float* kern, int up, int down, int width, int K,
+                           float* out, long Tout, void* stream) {
+    ZK_REQUIRE(up > 0 && down > 0 && K > 0 && width >= 0 && T >= 0 && Tout >= 0, "zk_resample: bad arguments");
+    if (B == 0 || Tout == 0) return 0;
+    hipLaunchKernelGGL(k_resample, dim3((unsigned)((Tout + 255) / 256), B), dim3(256), 0, (hipStream_t)stream, x, T,
+                       kern, up, down, width, K, out, Tout);
+    ZK_CHECK_LAUNCH("zk_resample");
+    return 0;
+}
 
 extern "C" int zk_loudness_gains(const float* wav, int B, long T, const int32_t* lens, int rate, double target_lufs,
                                  double* scratch, double* gains, double* loudness, void* stream) {
