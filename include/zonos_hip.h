@@ -270,6 +270,33 @@ int zk_dac_rvq_encode(const float* z, int B, int T, int hidden, int ncb, int nco
 int zk_resample(const float* x, int B, long T, const float* kern, int up, int down, int width, int K,
                 float* out, long Tout, void* stream);
 
+/* ---- PrefixConditioner.forward (zonos/conditioning.py:373-389; Zonos.prepare_conditioning,
+ * model.py:210-218): conditioner rows -> concat over the sequence -> prefix projection ->
+ * LayerNorm, one launch, out bf16 [B][L][D]. A plan lists the segments in the conditioners'
+ * order; a segment's input batch `bin` is 1 (broadcast, the reference's expand) or B. */
+#define ZK_COND_MAXSEG 16
+#define ZK_COND_MAXIN 64
+enum { ZK_SEG_VECTOR = 0,   /* learned uncond vector: table bf16 [D], len 1 */
+       ZK_SEG_EMBED = 1,    /* embedding: input int64 ids [bin][in_bstride], row = table[id - id_min] */
+       ZK_SEG_FOURIER = 2,  /* Fourier: input fp32 [bin][len][in_dim], table = W bf16 [cin/2][in_dim] */
+       ZK_SEG_PASS = 3 };   /* passthrough: input bf16 [bin][len][cin] */
+typedef struct {
+    int type, len, cin, in_dim, bin, proj;   /* proj: 0 none, 1 linear, 2 mlp (conditioning.py:27-34) */
+    long in_bstride, id_min;
+    float vmin, vden;                        /* Fourier: (x - vmin) / vden */
+    const void* table;
+    const void* input;
+    const void* pw0; const void* pb0; const void* pw1; const void* pb1;   /* bf16 projection [D][cin], [D][D] */
+} ZkCondSeg;
+typedef struct {
+    int nseg, D, L, proj;
+    float eps;
+    const void* pw0; const void* pb0; const void* pw1; const void* pb1;   /* prefix projection */
+    const void* norm_w; const void* norm_b;                                /* LayerNorm (NULL: none) */
+    ZkCondSeg seg[ZK_COND_MAXSEG];
+} ZkCondPlan;
+int zk_prefix_cond(const ZkCondPlan* plan, int B, void* out, void* stream);
+
 /* ------------------------------------------------------------------ hybrid backbone: Mamba2 mixer
  * (zonos/backbone/_mamba_ssm.py -> mamba_ssm Mamba2; restated in oracle/hybrid_ref.py).
  * in_proj output columns [z (d_inner) | xBC (conv_dim = d_inner + 2 d_state) | dt (nheads)].

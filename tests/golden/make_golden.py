@@ -345,13 +345,58 @@ def make_dac_encoder_fixture():
                         codes=codes.numpy().astype(np.int16), seed=np.int64(seed))
 
 
+def make_cond_fixtures():
+    """PrefixConditioner.forward / Zonos.prepare_conditioning (conditioning.py:373-389,
+    model.py:210-218) run by the reference module, bf16, D=256; phonemize replaced by a fixed
+    text -> IPA table (eSpeak is absent)."""
+    import zonos.conditioning as zc
+    from zonos.config import PrefixConditionerConfig
+
+    from oracle import cond_ref
+    from tests.golden_util import COND_CASES, COND_PHONEMES
+    D = 256
+    out = {}
+    for name, (kind, proj, texts, kw, with_spk, cproj) in COND_CASES.items():
+        conds = [dict(c) for c in (cond_ref.TRANSFORMER_CONDITIONERS if kind == "transformer"
+                                   else cond_ref.HYBRID_CONDITIONERS)]
+        for c in conds:
+            if cproj and c["name"] in cproj:
+                c["projection"] = cproj[c["name"]]
+        W = cond_ref.make_weights(conds, D, proj, seed=3)
+        pc = zc.PrefixConditioner(PrefixConditionerConfig(conds, proj), D).to(torch.bfloat16)
+        sd = pc.state_dict()
+        assert set(sd) == set(W), (set(sd) ^ set(W))
+        pc.load_state_dict(W)
+        pc.eval()
+        zc.phonemize = lambda t, l: [COND_PHONEMES[x] for x in t]
+        spk = (torch.randn(1, 128, generator=torch.Generator().manual_seed(9)).bfloat16() if with_spk else None)
+        cd = zc.make_cond_dict(text=texts, speaker=spk, device="cpu", **kw)
+        unc = {k: cd[k] for k in pc.required_keys}
+        with torch.no_grad():
+            y = torch.cat([pc(cd), pc(unc)])
+            ids, _ = zc.tokenize_phonemes([COND_PHONEMES[x] for x in texts])
+            y_o = torch.cat([cond_ref.prefix_conditioner(W, conds, cd, ids, proj),
+                             cond_ref.prefix_conditioner(W, conds, unc, ids, proj)])
+        print(f"[cond {name}] {tuple(y.shape)} oracle bit-exact {torch.equal(y, y_o)}")
+        assert torch.equal(y, y_o)
+        out[f"{name}_y"] = y.view(torch.int16).numpy()
+        out[f"{name}_ids"] = ids.numpy()
+        if spk is not None:
+            out[f"{name}_spk"] = spk.view(torch.int16).numpy()
+    np.savez_compressed(os.path.join(HERE, "cond.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     if len(sys.argv) > 1 and sys.argv[1] == "enc":
         make_dac_encoder_fixture()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "cond":
+        make_cond_fixtures()
         sys.exit(0)
     make_delay_fixtures()
     make_sampler_fixtures()
     make_generate_fixtures()
     make_dac_fixtures()
     make_dac_encoder_fixture()
+    make_cond_fixtures()

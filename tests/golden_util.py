@@ -46,3 +46,41 @@ def load_gen_case(name):
                 max_new=int(d["max_new"]), seed=int(d["seed"]), sp=sp, codes=d["codes"], lens=d["lens"],
                 delayed=d["delayed"], offset=int(d["offset"]),
                 logits=d["logits"] if "logits" in d.files else None)
+
+
+# ---- PrefixConditioner fixtures (cond.npz; made by make_golden.make_cond_fixtures)
+COND_PHONEMES = {"hello": "həlˈoʊ wˈɜːld!", "long": "ðɪs ɪz ə lˈɔŋɡɚ sˈɛntəns, wɪð pˈʌŋktʃuːˈeɪʃən… ænd ɐ ʔ",
+                 "unk": "a1b"}
+COND_CASES = {
+    # name: (conditioner list, prefix projection, texts, cond_dict kwargs, speaker?, per-conditioner projection)
+    "transformer_default": ("transformer", "none", ["hello", "long"], {}, True, None),
+    "hybrid_all_cond": ("hybrid", "none", ["long"], dict(unconditional_keys=[], speaker_noised=True, fmax=24000.0,
+                                                      language="ja", emotion=[0.3, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1],
+                                                      pitch_std=80.0, speaking_rate=22.5, ctc_loss=3.0,
+                                                      dnsmos_ovrl=3.5, vqscore_8=[0.7, 0.72, 0.74, 0.76, 0.78,
+                                                                                  0.8, 0.79, 0.6]), False, None),
+    "projections": ("transformer", "mlp", ["unk", "hello"], dict(unconditional_keys=["emotion"]), True,
+                    {"fmax": "mlp", "language_id": "linear"}),
+}
+
+
+def cond_case(name: str, device="cpu"):
+    """Rebuild a cond.npz case: conditioner configs, projection, weights, cond / uncond dicts (on
+    ``device``, built by zonos_amd.conditioning.make_cond_dict), phoneme ids, expected [2B, L, D]."""
+    from oracle import cond_ref
+    from zonos_amd import conditioning as zc
+    d = np.load(os.path.join(G, "cond.npz"))
+    kind, proj, texts, kw, with_spk, cproj = COND_CASES[name]
+    conds = [dict(c) for c in (cond_ref.TRANSFORMER_CONDITIONERS if kind == "transformer"
+                               else cond_ref.HYBRID_CONDITIONERS)]
+    for c in conds:
+        if cproj and c["name"] in cproj:
+            c["projection"] = cproj[c["name"]]
+    W = cond_ref.make_weights(conds, 256, proj, seed=3)
+    spk = torch.from_numpy(d[f"{name}_spk"]).view(torch.bfloat16) if with_spk else None
+    cd = zc.make_cond_dict(text=texts, speaker=spk, device=device, **kw)
+    required = {c["name"] for c in conds if c.get("uncond_type", "none") != "learned"}
+    unc = {k: cd[k] for k in required}
+    phon = [COND_PHONEMES[t] for t in texts]
+    return dict(conds=conds, proj=proj, W=W, cond=cd, uncond=unc, texts=texts, phonemes=phon,
+                ids=torch.from_numpy(d[f"{name}_ids"]), y=torch.from_numpy(d[f"{name}_y"]).view(torch.bfloat16))

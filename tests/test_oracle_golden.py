@@ -10,7 +10,7 @@ import torch
 from oracle import dac_ref, zonos_ref
 from oracle.philox import exp_noise, philox4x32_10
 
-from .golden_util import ENC_DAC, GEN_CASES, TINY, TINY_DAC, load_enc_case, load_gen_case, wsum
+from .golden_util import COND_CASES, ENC_DAC, cond_case, GEN_CASES, TINY, TINY_DAC, load_enc_case, load_gen_case, wsum
 
 G = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -92,3 +92,17 @@ def test_dac_encoder_golden():
         z, codes = dac_ref.encode(W, ENC_DAC, wav)
     assert (z - z_ref).abs().max().item() < 1e-4
     assert torch.equal(codes, codes_ref)
+
+
+@pytest.mark.parametrize("name", list(COND_CASES))
+def test_prefix_conditioner_golden(name):
+    """oracle PrefixConditioner (fed by zonos_amd's make_cond_dict + phoneme tokenizer) == the
+    reference module's prepare_conditioning output (cond.npz), bit for bit."""
+    from oracle import cond_ref
+    from zonos_amd.conditioning import tokenize_phonemes
+    c = cond_case(name, "cpu")
+    ids, _ = tokenize_phonemes(c["phonemes"])
+    assert torch.equal(ids, c["ids"])
+    y = torch.cat([cond_ref.prefix_conditioner(c["W"], c["conds"], c["cond"], ids, c["proj"]),
+                   cond_ref.prefix_conditioner(c["W"], c["conds"], c["uncond"], ids, c["proj"])])
+    assert torch.equal(y, c["y"])

@@ -78,6 +78,7 @@ _SIGS = {
     "zk_dac_enc_conv1": [P, I, I, P, P, P, I, I, P, P, P],
     "zk_dac_rvq_encode": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P],
     "zk_resample": [P, I, L, P, I, I, I, I, P, L, P],
+    "zk_prefix_cond": [P, I, P, P],
     "zk_loudness_gains": [P, I, L, P, I, C.c_double, P, P, P, P],
 }
 

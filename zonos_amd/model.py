@@ -4,8 +4,9 @@ Kept from the reference: ``Zonos.from_pretrained`` / ``from_local`` / ``generate
 ``autoencoder`` / ``embed_codes`` semantics and the same safetensors key names
 (backbone.layers.{i}.{norm,mixer.in_proj,mixer.out_proj,norm2,mlp.fc1,mlp.fc2},
 backbone.norm_f, embeddings.{k}, heads.{k}). The text/speaker front end
-(prepare_conditioning, make_speaker_embedding) is outside this engine's scope: callers
-pass the [2B, Lc, D] prefix conditioning produced by the reference's PrefixConditioner.
+``prepare_conditioning`` runs the PrefixConditioner as one HIP launch (zonos_amd/conditioning.py);
+the eSpeak phonemizer and the speaker-embedding network (make_speaker_embedding) are outside this
+engine's scope.
 """
 from __future__ import annotations
 
@@ -40,6 +41,11 @@ class Zonos:
         else:
             self.engine = HipDecoder(EngineConfig.from_backbone_config(bc), state_dict, self.device)
         self._autoencoder = autoencoder
+        pc = {k[len("prefix_conditioner."):]: v for k, v in state_dict.items() if k.startswith("prefix_conditioner.")}
+        self.prefix_conditioner = None
+        if pc:
+            from .conditioning import PrefixConditioner
+            self.prefix_conditioner = PrefixConditioner(config.prefix_conditioner, bc.d_model, pc, self.device)
 
     @property
     def autoencoder(self) -> DACAutoencoder:
@@ -65,13 +71,15 @@ class Zonos:
         sd = {}
         with safe_open(model_path, framework="pt") as f:
             for k in f.keys():
-                if k.startswith(("backbone.", "embeddings.", "heads.")):
+                if k.startswith(("backbone.", "embeddings.", "heads.", "prefix_conditioner.")):
                     sd[k] = f.get_tensor(k)
         return cls(config, sd, device, autoencoder)
 
     def prepare_conditioning(self, cond_dict: dict, uncond_dict: dict | None = None) -> torch.Tensor:
-        raise NotImplementedError("PrefixConditioner (zonos/conditioning.py) is outside the HIP engine's scope; "
-                                  "pass the [2B, Lc, d_model] prefix conditioning to generate()")
+        """model.py:210-218: [2B, L, d_model] bf16 = cat(PrefixConditioner(cond), PrefixConditioner(uncond))."""
+        if self.prefix_conditioner is None:
+            raise ValueError("this model was loaded without prefix_conditioner.* weights")
+        return self.prefix_conditioner.prepare_conditioning(cond_dict, uncond_dict)
 
     def make_speaker_embedding(self, wav, sr):
         raise NotImplementedError("speaker embedding (zonos/speaker_cloning.py) is outside the HIP engine's scope")
