@@ -200,7 +200,14 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
 constexpr int WS_NB = ZK_WS_NB;  // LDS ring slots (16 KB each)
 constexpr int WS_DA = ZK_WS_DA;  // activation chunks in flight (loader); WS_NB >= WS_DA + 2
 constexpr int WS_THREADS = 320;
-constexpr int WS_PF = 4;         // weight chunks in flight per compute wave
+#ifndef ZK_WS_PF
+#define ZK_WS_PF 4
+#endif
+#ifndef ZK_WS_NT
+#define ZK_WS_NT 0
+#endif
+constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
+constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 
 template <int N_>
 ZK_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
@@ -271,14 +278,14 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
         const int pc = p < NCH ? p : NCH - 1;
-        wr0[p] = ldg_w<false>(wrow + pc * WCH);
-        wr1[p] = ldg_w<false>(wrow + pc * WCH + WHALF);
+        wr0[p] = ldg_w<WS_NT>(wrow + pc * WCH);
+        wr1[p] = ldg_w<WS_NT>(wrow + pc * WCH + WHALF);
     }
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
         if (ch + PF < NCH) {
-            wr0[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * WCH);
-            wr1[(ch + PF) % U] = ldg_w<false>(wrow + (ch + PF) * WCH + WHALF);
+            wr0[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH);
+            wr1[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH + WHALF);
         }
         __builtin_amdgcn_s_barrier();                               // chunk ch is in LDS
         asm volatile("" ::: "memory");
