@@ -78,3 +78,27 @@ def test_kv_layout_pack_roundtrip():
         for ch in (0, 17, 127):
             off = (key >> 5) * 4096 + ((ch >> 4) * 64 + (o >> 3) * 16 + (ch & 15)) * 8 + (o & 7)
             assert vp[1, 2, off] == v[1, 2, key, ch]
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors of the by-value/by-pointer structs (ZkCondPlan, sampling params, generation
+    state) have the C compiler's size and field offsets."""
+    import ctypes as C
+    import shutil
+    import subprocess
+
+    from zonos_amd import _lib as zl
+    from zonos_amd.conditioning import ZkCondPlan, ZkCondSeg
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "zonos_hip.h")
+    src = tmp_path / "layout.c"
+    src.write_text(f'#include "{hdr}"\n#include <stdio.h>\n#include <stddef.h>\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(ZkCondSeg), sizeof(ZkCondPlan),'
+                   ' offsetof(ZkCondPlan, seg), offsetof(ZkCondSeg, table), offsetof(ZkCondPlan, norm_w),'
+                   ' sizeof(zk_sampling_params)); return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [C.sizeof(ZkCondSeg), C.sizeof(ZkCondPlan), ZkCondPlan.seg.offset, ZkCondSeg.table.offset,
+                   ZkCondPlan.norm_w.offset, C.sizeof(zl.SamplingParams)]
