@@ -76,7 +76,7 @@ def test_delay_pattern_golden():
 
 @pytest.mark.parametrize("M,N,K,nsplit", [(128, 3072, 2048, 8), (7, 1026 * 9, 256, 2), (300, 192, 512, 1),
                                           (128, 2048, 8192, 16), (2, 2048, 2048, 4), (20, 3072, 1024, 2),
-                                          (64, 1168, 256, 4)])
+                                          (64, 1168, 256, 4), (128, 3072, 2048, 1), (33, 1024, 8192, 1)])
 def test_gemm_vs_fp32(M, N, K, nsplit):
     from zonos_amd._lib import call, ptr, stream_ptr
     g = torch.Generator(device="cpu").manual_seed(M + N)
@@ -109,10 +109,10 @@ def test_pack_weights_layout():
                 assert torch.equal(P[nt, kc, lane], exp)
 
 
-@pytest.mark.parametrize("M", [130, 2, 40])
-def test_gemm_swiglu(M):
+@pytest.mark.parametrize("M,Fd,D", [(130, 256, 512), (2, 256, 512), (40, 256, 512), (128, 512, 2048),
+                                    (3, 512, 2048)])
+def test_gemm_swiglu(M, Fd, D):
     from zonos_amd._lib import call, ptr, stream_ptr
-    Fd, D = 256, 512
     g = torch.Generator(device="cpu").manual_seed(1)
     A = torch.randn(M, D, generator=g).to(torch.bfloat16)
     W1 = (torch.randn(2 * Fd, D, generator=g) / D ** 0.5).to(torch.bfloat16)

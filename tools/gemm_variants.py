@@ -13,6 +13,9 @@ VARIANTS = {
     "pf8nt": {"ZK_WS_PF": 8, "ZK_WS_NT": 1},
     "pf6nt": {"ZK_WS_PF": 6, "ZK_WS_NT": 1},
     "occ2": {"ZK_WS_NB": 4, "ZK_WS_DA": 2, "ZK_WS_OCC": 2, "ZK_WS_NT": 1},
+    "ws2": {"ZK_WS2_MIN_CHUNKS": 32},
+    "ws2nt": {"ZK_WS2_MIN_CHUNKS": 32, "ZK_WS_NT": 1},
+    "ws2pf6nt": {"ZK_WS2_MIN_CHUNKS": 32, "ZK_WS_NT": 1, "ZK_WS_PF": 6},
 }
 if __name__ == "__main__":
     shutil.rmtree(os.path.join(LIBDIR, "variants"), ignore_errors=True)
