@@ -16,6 +16,8 @@ VARIANTS = {
     "ws2": {"ZK_WS2_MIN_CHUNKS": 32},
     "ws2nt": {"ZK_WS2_MIN_CHUNKS": 32, "ZK_WS_NT": 1},
     "ws2pf6nt": {"ZK_WS2_MIN_CHUNKS": 32, "ZK_WS_NT": 1, "ZK_WS_PF": 6},
+    "ws2all": {"ZK_WS2_MIN_CHUNKS": 8},
+    "ws2allnt": {"ZK_WS2_MIN_CHUNKS": 8, "ZK_WS_NT": 1},
 }
 if __name__ == "__main__":
     shutil.rmtree(os.path.join(LIBDIR, "variants"), ignore_errors=True)

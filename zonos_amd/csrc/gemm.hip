@@ -356,13 +356,14 @@ constexpr int WS2_THREADS = 576;
 template <int MODE, int NCHH, int PF, int MT>
 __global__ __launch_bounds__(WS2_THREADS, 1) void k_gemm_ws2(const bf16_t* __restrict__ A, long lda,
                                                           const bf16_t* __restrict__ W, int M, int N, int K,
-                                                          float* __restrict__ Cpart, bf16_t* __restrict__ Cout,
-                                                          const int32_t* skip) {
+                                                          int kslice, float* __restrict__ Cpart,
+                                                          bf16_t* __restrict__ Cout, const int32_t* skip) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip && *skip) return;
     constexpr int TILE = MT * 16 * BK * 2;            // bytes of one half's chunk
-    const int n0 = blockIdx.x * BN;
-    const int khalf_len = K / 2;
+    const int n0 = blockIdx.x * BN, split = blockIdx.z;
+    const int kbeg = split * kslice;
+    const int khalf_len = kslice / 2;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int ln = lane & 15, lg = lane >> 4;
 
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(WS2_THREADS, 1) void k_gemm_ws2(const bf16_t* __res
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 char* dst = smem + (ch % WS2_NB) * (2 * TILE) + h * TILE;
-                const int k0 = h * khalf_len + ch * BK;
+                const int k0 = kbeg + h * khalf_len + ch * BK;
 #pragma unroll
                 for (int i = 0; i < NP; ++i) {
                     const int row = 8 * i + rl;
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(WS2_THREADS, 1) void k_gemm_ws2(const bf16_t* __res
     const int cg = w & 3, kh = w >> 2;
     const int wn = n0 + cg * 16 + ln;
     const bool wvalid = wn < N;
-    const bf16_t* wrow = w_base(W, n0 + cg * 16, wvalid ? wn : 0, K, kh * khalf_len, lane);
+    const bf16_t* wrow = w_base(W, n0 + cg * 16, wvalid ? wn : 0, K, kbeg + kh * khalf_len, lane);
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -455,7 +456,7 @@ __global__ __launch_bounds__(WS2_THREADS, 1) void k_gemm_ws2(const bf16_t* __res
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int m = mt * 16 + lg * 4 + i;
-                    if (m < M) Cpart[(size_t)m * N + wn] = acc[mt][i];
+                    if (m < M) Cpart[(size_t)split * M * N + (size_t)m * N + wn] = acc[mt][i];
                 }
         }
     } else {
@@ -523,17 +524,18 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
 #ifndef ZK_WS2_MIN_CHUNKS
 #define ZK_WS2_MIN_CHUNKS 1000000
 #endif
-    if (M <= BM && nsplit == 1 && nchunks >= ZK_WS2_MIN_CHUNKS && nchunks <= 128 && nchunks % 2 == 0) {
+    if (M <= BM && nchunks >= ZK_WS2_MIN_CHUNKS && nchunks <= 128 && nchunks % 2 == 0) {
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
         const size_t lds = std::max<size_t>((size_t)WS2_NB * 2 * MT * 16 * BK * 2, (size_t)4 * MT * 64 * 16);
-        dim3 g((N + BN - 1) / BN);
+        dim3 g((N + BN - 1) / BN, 1, nsplit);
         bool handled = false;
 #define ZK_WS2_LAUNCH3(MODE_, NCHH_, MT_)                                                                          \
     do {                                                                                                          \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws2<MODE_, NCHH_, WS_PF, MT_>),          \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                \
         hipLaunchKernelGGL((k_gemm_ws2<MODE_, NCHH_, WS_PF, MT_>), g, dim3(WS2_THREADS), lds, (hipStream_t)stream, \
-                           (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, Cpart, (bf16_t*)Cout, skip_flag);     \
+                           (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,     \
+                           skip_flag);                                                                             \
         handled = true;                                                                                           \
     } while (0)
 #define ZK_WS2_LAUNCH(MODE_, NCHH_)                                                                                \
@@ -547,8 +549,9 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     } while (0)
         if (mode == 0) {
             switch (nchunks / 2) {
+                case 4: ZK_WS2_LAUNCH(0, 4); break;
+                case 8: ZK_WS2_LAUNCH(0, 8); break;
                 case 16: ZK_WS2_LAUNCH(0, 16); break;
-                case 64: ZK_WS2_LAUNCH(0, 64); break;
                 default: break;
             }
         } else {
