@@ -204,7 +204,7 @@ constexpr int WS_THREADS = 320;
 #define ZK_WS_PF 4
 #endif
 #ifndef ZK_WS_NT
-#define ZK_WS_NT 0
+#define ZK_WS_NT 1
 #endif
 constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads

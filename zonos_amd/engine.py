@@ -19,6 +19,7 @@ Design (MI355X-first):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -80,6 +81,12 @@ def _split_for(N: int, K: int, M: int, target_blocks: int = 256) -> int:
         if K % (cand * 64) == 0:
             s = cand
     return s
+
+
+def _split_overrides() -> dict:
+    """Tuning knob (not used by default): ZK_SPLITS="qkv=4,o=4,fc2=4" fixes split-K counts."""
+    env = os.environ.get("ZK_SPLITS", "")
+    return {k: int(v) for k, v in (kv.split("=") for kv in env.split(",") if kv)}
 
 
 def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> int:
@@ -158,6 +165,7 @@ class HipDecoder:
         f32, bf, i32 = torch.float32, torch.bfloat16, torch.int32
         splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R), fc2=_split_for(D, Fd, R),
                       heads=_split_for(Nh, D, R))
+        splits.update(_split_overrides())
         part_n = max(Mp * Nqkv, Mp * D, splits["qkv"] * R * Nqkv, splits["o"] * R * D, splits["fc2"] * R * D,
                      splits["heads"] * R * Nh)
         attn_splits = attn_splits_for(R, Hk, smax)
