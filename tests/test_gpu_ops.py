@@ -240,14 +240,17 @@ def test_attention_prefill(R, S, H, Hk):
     hd = 128
     smax = ((S + 255) // 256) * 256
     k, v, kc, vt = _attn_setup(R, S, H, Hk, hd, smax, seed=3)
-    q = torch.randn(R, S, H, hd).to(torch.bfloat16)
+    q = torch.randn(R, S, H, hd, generator=torch.Generator().manual_seed(4)).to(torch.bfloat16)
     ref = F.scaled_dot_product_attention(q.transpose(1, 2).float(), k.transpose(1, 2).float(),
                                          v.transpose(1, 2).float(), is_causal=S > 1, enable_gqa=True)
     ref = ref.transpose(1, 2).reshape(R * S, H * hd)
     out = torch.empty(R * S, H * hd, dtype=torch.bfloat16, device=DEV)
     qd, kd, vd = q.reshape(R * S, H * hd).to(DEV), kc.to(DEV), vt.to(DEV)
     call("zk_attn_prefill", ptr(qd), ptr(kd), ptr(vd), R, S, H, Hk, hd, smax, ptr(out), stream_ptr())
-    assert (out.float().cpu() - ref).abs().max() < 1e-2
+    # P is rounded to bf16 before P.V (as the reference's CPU flash kernel does) and the output is
+    # bf16: vs an fp32 SDPA that is up to ~1 bf16 ulp of |out| <= ~2 per element, mean far below.
+    err = (out.float().cpu() - ref).abs()
+    assert err.max() < 2e-2 and err.mean() < 2e-3, (err.max(), err.mean())
 
 
 def test_qkv_rope_matches_oracle():
