@@ -76,7 +76,10 @@ def test_delay_pattern_golden():
 
 @pytest.mark.parametrize("M,N,K,nsplit", [(128, 3072, 2048, 8), (7, 1026 * 9, 256, 2), (300, 192, 512, 1),
                                           (128, 2048, 8192, 16), (2, 2048, 2048, 4), (20, 3072, 1024, 2),
-                                          (64, 1168, 256, 4), (128, 3072, 2048, 1), (33, 1024, 8192, 1)])
+                                          (64, 1168, 256, 4), (128, 3072, 2048, 1), (33, 1024, 8192, 1),
+                                          # k_gemm_rk shapes (decode, M <= 128): 4- and 2-tile workgroups
+                                          (128, 2048, 2048, 8), (128, 9234, 2048, 2), (128, 16384, 2048, 1),
+                                          (128, 2048, 2048, 4), (100, 2048, 8192, 4), (1, 3072, 2048, 2)])
 def test_gemm_vs_fp32(M, N, K, nsplit):
     from zonos_amd._lib import call, ptr, stream_ptr
     g = torch.Generator(device="cpu").manual_seed(M + N)

@@ -11,6 +11,9 @@ VARIANTS = {
     "nt_noa": {"ZK_WS_NT": 1, "ZK_DBG_NOALOAD": 1},
     "nt_nom": {"ZK_WS_NT": 1, "ZK_DBG_NOMFMA": 1},
     "nt_noboth": {"ZK_WS_NT": 1, "ZK_DBG_NOALOAD": 1, "ZK_DBG_NOMFMA": 1},
+    "ws2all": {"ZK_WS2_MIN_CHUNKS": 8},
+    "occ2": {"ZK_WS_NB": 4, "ZK_WS_DA": 2, "ZK_WS_OCC": 2},
+    "pf8": {"ZK_WS_PF": 8},
 }
 if __name__ == "__main__":
     shutil.rmtree(os.path.join(LIBDIR, "variants"), ignore_errors=True)

@@ -41,6 +41,8 @@ def gemm():
         Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]   # packed-size buffers
         A = torch.randn(M, K, device=dev).to(torch.bfloat16)
         ns = 1 if mode == 1 else _split_for(N, K, M, int(os.environ.get("ZK_SPLIT_TARGET", "256")))
+        ovr = dict(kv.split("=") for kv in os.environ.get("ZK_SPLITS", "").split(",") if kv)
+        ns = int(ovr.get(name, ns))
         part = torch.empty(ns * M * N, device=dev)
         out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
         it = [0]

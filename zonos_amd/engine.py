@@ -163,8 +163,9 @@ class HipDecoder:
         Nh = N_CB * VOCAB
         Mp = R * S_pre
         f32, bf, i32 = torch.float32, torch.bfloat16, torch.int32
-        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R), fc2=_split_for(D, Fd, R),
-                      heads=_split_for(Nh, D, R))
+        # heads: no split-K (145 workgroups of 64 columns stream 37.8 MB in 15.6 us vs 19.8 us
+        # with 2 splits, tools/microbench.py gemm; the sampler then reads one slab)
+        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R), fc2=_split_for(D, Fd, R), heads=1)
         splits.update(_split_overrides())
         part_n = max(Mp * Nqkv, Mp * D, splits["qkv"] * R * Nqkv, splits["o"] * R * D, splits["fc2"] * R * D,
                      splits["heads"] * R * Nh)
