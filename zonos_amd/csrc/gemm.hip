@@ -199,13 +199,21 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
 #endif
 constexpr int WS_NB = ZK_WS_NB;  // LDS ring slots (16 KB each)
 constexpr int WS_DA = ZK_WS_DA;  // activation chunks in flight (loader); WS_NB >= WS_DA + 2
-constexpr int WS_THREADS = 320;
+#ifndef ZK_WS_NLD
+#define ZK_WS_NLD 4
+#endif
+constexpr int WS_NLD = ZK_WS_NLD;            // loader waves (each moves 1/WS_NLD of every chunk)
+constexpr int WS_THREADS = 256 + 64 * WS_NLD;
 #ifndef ZK_WS_PF
 #define ZK_WS_PF 4
 #endif
 #ifndef ZK_WS_NT
 #define ZK_WS_NT 1
 #endif
+#ifndef ZK_WS_LDSPF
+#define ZK_WS_LDSPF 1
+#endif
+constexpr int WS_LDSPF = ZK_WS_LDSPF;   // chunks published ahead of the one being multiplied
 constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 
@@ -227,17 +235,21 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int ln = lane & 15, lg = lane >> 4;
 
-    if (w == 4) {
-        // ---------------- loader wave: 2*MT x 1 KB LDS-DMA pieces per chunk (16*MT rows x 64 k)
+    if (w >= 4) {
+        // ---------------- loader wave(s): 2*MT x 1 KB LDS-DMA pieces per chunk (16*MT rows x 64 k),
+        // loader l moving pieces l, l + WS_NLD, ...
         // piece i covers tile rows 8i..8i+7; lane L lands at byte 16L of the piece:
         // row = 8i + (L>>3), slot = L&7  ->  source 16-B chunk = slot ^ (row&7)
-        constexpr int NP = 2 * MT;
+        constexpr int NP = (2 * MT + WS_NLD - 1) / WS_NLD;      // pieces per loader per chunk
+        const int ld = w - 4;
         const int rl = lane >> 3, sl = lane & 7;
         auto issue = [&](int ch) {
             char* dst = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
             const int k0 = kbeg + ch * BK;
 #pragma unroll
-            for (int i = 0; i < NP; ++i) {
+            for (int j = 0; j < NP; ++j) {
+                const int i = j * WS_NLD + ld;
+                if (WS_NLD > 1 && i >= 2 * MT) break;          // (MT = 1, 2 loaders: 1 piece each)
                 const int row = 8 * i + rl;
                 const int m = min(row, M - 1);
                 const bf16_t* src = A + (size_t)m * lda + k0 + ((sl ^ (row & 7)) << 3);
@@ -251,14 +263,17 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         const int pre = min(WS_DA, nchunks);
         for (int c = 0; c < pre; ++c) issue(c);
         for (int c = 0; c < nchunks; ++c) {
-            const int younger = min(c + WS_DA, nchunks) - c - 1;     // chunks issued after c
+            // barrier c publishes chunk `need` (ZK_WS_LDSPF: one chunk ahead, so the compute
+            // waves can read chunk c+1's fragments while they multiply chunk c)
+            const int need = min(c + WS_LDSPF, nchunks - 1);
+            const int younger = min(c - 1 + WS_DA, nchunks - 1) - need;   // chunks issued after `need`
             if (younger >= 3) vm_wait<3 * NP>();
             else if (younger == 2) vm_wait<2 * NP>();
             else if (younger == 1) vm_wait<NP>();
             else vm_wait<0>();
-            __builtin_amdgcn_s_barrier();                           // publish chunk c
+            __builtin_amdgcn_s_barrier();                           // publish chunk `need`
             asm volatile("" ::: "memory");
-            if (c + WS_DA < nchunks) issue(c + WS_DA);              // its slot was read 2 chunks ago
+            if (c + WS_DA < nchunks) issue(c + WS_DA);              // its slot was read >= 2 chunks ago
         }
         return;
     }
@@ -281,6 +296,42 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         wr0[p] = ldg_w<WS_NT>(wrow + pc * WCH);
         wr1[p] = ldg_w<WS_NT>(wrow + pc * WCH + WHALF);
     }
+#if ZK_WS_LDSPF
+    // activation fragments of the next chunk are read from LDS (register double buffer) while
+    // the current chunk is multiplied: the LDS latency after each barrier is off the MFMA path
+    uint4 af[2][2][MT];
+    auto read_frags = [&](int ch, int buf) {
+        const char* base = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                af[buf][ks][mt] = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
+    };
+    __builtin_amdgcn_s_barrier();                                   // chunk 0 (and 1) in LDS
+    asm volatile("" ::: "memory");
+    read_frags(0, 0);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + PF < NCH) {
+            wr0[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH);
+            wr1[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH + WHALF);
+        }
+        if (ch + 1 < NCH) {
+            __builtin_amdgcn_s_barrier();                           // chunk ch+1 (and ch+2) in LDS
+            asm volatile("" ::: "memory");
+            read_frags(ch + 1, (ch + 1) & 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);     // keep the fragment reads ahead of this chunk's MFMAs
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(af[ch & 1][ks][mt]), b, acc[mt], 0, 0, 0);
+        }
+    }
+#else
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
         if (ch + PF < NCH) {
@@ -309,6 +360,7 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
             }
         }
     }
+#endif
     if (MODE == 0) {
         float* C = Cpart + (size_t)split * M * N;
         if (wvalid) {
