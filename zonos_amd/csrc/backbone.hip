@@ -78,6 +78,7 @@ ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, 
 constexpr int LN_NT = 256;
 constexpr int RL_MAXS = 8;    // split-K slabs k_resid_ln reduces with all loads in flight
 constexpr int MAX_N8 = 4;     // D <= 8192
+constexpr int EMB_MAXK = 9;   // codebooks summed by k_embed_ln (Zonos: 9)
 
 template <int N8>
 __global__ __launch_bounds__(LN_NT) void k_embed_ln(const int64_t* ids, int B, int S, int K, long bstr, long kstr,
@@ -91,16 +92,28 @@ __global__ __launch_bounds__(LN_NT) void k_embed_ln(const int64_t* ids, int B, i
     const int col = t + (col_dev ? *col_dev + col_add : 0);
     constexpr int n8 = N8;
     float x[N8 * 8];
+    // all code ids, then all embedding rows, issued before the first add (two memory round
+    // trips per step instead of 2K dependent ones); K <= EMB_MAXK (host-checked)
+    int64_t idv[EMB_MAXK];
+#pragma unroll
+    for (int k = 0; k < EMB_MAXK; ++k) {
+        int64_t id = k < K ? ids[b * bstr + k * kstr + col] : 0;
+        idv[k] = id < 0 ? 0 : (id >= V ? V - 1 : id);
+    }
 #pragma unroll
     for (int j = 0; j < n8; ++j) {
         const int c = (threadIdx.x + LN_NT * j) * 8;
         if (c >= D) continue;
         float acc[8];
-        for (int k = 0; k < K; ++k) {
-            int64_t id = ids[b * bstr + k * kstr + col];
-            id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+        uint4 ev[EMB_MAXK];
+#pragma unroll
+        for (int k = 0; k < EMB_MAXK; ++k)
+            if (k < K) ev[k] = *reinterpret_cast<const uint4*>(emb + ((size_t)k * V + idv[k]) * D + c);
+#pragma unroll
+        for (int k = 0; k < EMB_MAXK; ++k) {
+            if (k >= K) break;
             float e[8];
-            unpack8(*reinterpret_cast<const uint4*>(emb + ((size_t)k * V + id) * D + c), e);
+            unpack8(ev[k], e);
 #pragma unroll
             for (int q = 0; q < 8; ++q) acc[q] = (k == 0) ? e[q] : round_bf(acc[q] + e[q]);
         }
@@ -395,7 +408,10 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     // that of reading the cache. The first key block can therefore be fetched before the prologue.
     const int pos = ctx - 1;
     const bool early = FUSED && kb1 > kb0;
-    if (early) load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
+    if (early) {      // the first TWO key blocks are in flight during the prologue
+        load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
+        load_kv(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
+    }
     if constexpr (FUSED) {
         // pairs: [0, G*64) q of heads g*G.., then 64 k pairs, then 64 v pairs
         const int N = (H + 2 * Hkv) * HD;
@@ -467,7 +483,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     if (kb1 > kb0) {
         if (!early) load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         for (int it = kb0; it < kb1; it += 2) {
-            load_kv(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
+            if (!(early && it == kb0)) load_kv(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
             if (FUSED) patch_kv(fa, s_kn, s_vn, it * AT_KB + 32 * w, pos, ln, lg);
             attn_step(st, fa, qf, it * AT_KB + 32 * w, ctx, scale, lg);
             load_kv(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
@@ -661,6 +677,7 @@ extern "C" int zk_embed_codes(const int64_t* ids, int B, int S, int K, long ids_
     ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_embed_codes: D=%d must be a multiple of 8 (<= %d)", D,
                8 * LN_NT * MAX_N8);
     ZK_REQUIRE(B > 0 && S > 0 && K > 0 && rows_dup > 0, "zk_embed_codes: empty shape");
+    ZK_REQUIRE(K <= EMB_MAXK, "zk_embed_codes: K=%d codebooks > %d", K, EMB_MAXK);
     const int rows = rows_dup * B * S;
     ZK_REQUIRE(out_S >= out_t0 + S, "zk_embed_codes: out_S=%d < out_t0+S", out_S);
     ZK_LN_DISPATCH(D, k_embed_ln, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, ids, B, S, K, ids_bstride,

@@ -20,6 +20,7 @@ constexpr int NPT = 5;          // values per lane: V <= 1280
 constexpr int SORTN = 2048;
 constexpr int MAXW = 512;       // repetition-penalty window held in LDS
 constexpr int EOS = 1024, MASK = 1025;
+constexpr int EOS_MAXK = 16;    // codebooks handled by k_eos_step's unrolled frame write
 // float32(log(1024)) as torch computes it (model.py:324)
 constexpr float LOG1024F = 6.931471824645996f;
 
@@ -300,13 +301,9 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
     if (scal[3]) return;                                    // generation finished
     int new_eos_b = 0;
     if (draw == 1) {   // EOS resample happens only if some row has a new EOS (model.py:380)
-        if (threadIdx.x == 0) {
-            int any = 0;
-            for (int r = 0; r < B; ++r) any |= (st.tok0[r * K] == EOS) && !st.eos_mode[r];
-            s.flag = any;
-        }
-        __syncthreads();
-        if (!s.flag) return;
+        int any = 0;   // one row per thread: a single memory round trip
+        for (int r = threadIdx.x; r < B; r += NT) any |= (st.tok0[r * K] == EOS) && !st.eos_mode[r];
+        if (!__syncthreads_or(any)) return;
         new_eos_b = (st.tok0[b * K] == EOS) && !st.eos_mode[b];
     }
     const size_t N = (size_t)K * V;
@@ -381,12 +378,22 @@ __global__ __launch_bounds__(NT) void k_eos_step(zk_gen_state st, int prefill, i
         if (tok[0] == EOS) { rem = min(rem, 9); st.stopping[b] = 1; }      // model.py:399-402
         const int stop = st.stopping[b];
         const int idx = min(9 - rem, K - 1);                               // model.py:405-406
-        for (int k = 0; k < K; ++k) {
-            int v = tok[k];
-            if (stop) v = k < idx ? MASK : (k == idx ? EOS : v);           // model.py:410-414
-            if (offset < Ld) {   // the reference's last iteration writes an empty slice
-                int64_t* d = st.delayed + ((size_t)b * K + k) * Ld + offset;
-                if (*d == -1) *d = v;                                      // model.py:417-418
+        if (offset < Ld) {       // the reference's last iteration writes an empty slice
+            // all K frame cells and tokens loaded before the first store (one round trip)
+            int64_t cur[EOS_MAXK];
+            int tv[EOS_MAXK];
+#pragma unroll
+            for (int k = 0; k < EOS_MAXK; ++k)
+                if (k < K) {
+                    cur[k] = st.delayed[((size_t)b * K + k) * Ld + offset];
+                    tv[k] = tok[k];
+                }
+#pragma unroll
+            for (int k = 0; k < EOS_MAXK; ++k) {
+                if (k >= K) break;
+                int v = tv[k];
+                if (stop) v = k < idx ? MASK : (k == idx ? EOS : v);       // model.py:410-414
+                if (cur[k] == -1) st.delayed[((size_t)b * K + k) * Ld + offset] = v;   // model.py:417-418
             }
         }
         rem -= 1;                                                          // model.py:424
@@ -460,6 +467,7 @@ extern "C" int zk_sample_heads(const float* part, int nsplit, const zk_gen_state
 
 extern "C" int zk_eos_step(const zk_gen_state* st, int prefill, int prefix_len, void* stream) {
     ZK_REQUIRE(st != nullptr, "zk_eos_step: null state");
+    ZK_REQUIRE(st->K <= EOS_MAXK, "zk_eos_step: K=%d codebooks > %d", st->K, EOS_MAXK);
     hipLaunchKernelGGL(k_eos_step, dim3(1), dim3(NT), 0, (hipStream_t)stream, *st, prefill, prefix_len);
     ZK_CHECK_LAUNCH("zk_eos_step");
     return 0;
