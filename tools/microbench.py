@@ -32,7 +32,7 @@ def timeit(fn, reps=50, warm=5):
 
 
 def gemm():
-    M = 128
+    M = int(os.environ.get("ZK_MB_M", "128"))
     for name, N, K, mode in (("qkv", 3072, 2048, 0), ("o", 2048, 2048, 0), ("fc1", 16384, 2048, 1),
                              ("fc2", 2048, 8192, 0), ("heads", 9234, 2048, 0)):
         # distinct weight buffers per rep set so L2/MALL does not serve them: rotate 8 copies (>256 MB total)

@@ -16,6 +16,7 @@
 #include "common.h"
 #include "../../include/zonos_hip.h"
 #include <algorithm>
+#include <stdlib.h>
 
 namespace {
 
@@ -529,6 +530,94 @@ __global__ __launch_bounds__(WS2_THREADS, 1) void k_gemm_ws2(const bf16_t* __res
     }
 }
 
+// ------------------------------------------------------------------ decode GEMV, M <= 16
+// Small batches (B = 1 decode: 2 rows) are a pure weight stream: one 16-row activation tile
+// per K step feeds NTW MFMAs, so nothing is staged through LDS and there are no barriers in
+// the main loop. The workgroup's 4 waves split the K range (wave w owns quarter w) and each
+// streams all NTW*16 columns of the tile for its quarter -- weights fragment-packed, nt, PF
+// k-steps in flight (sched_barrier-pinned), the activation fragment from L2. The quarters are
+// summed through LDS in a fixed order (q0 + q1 + q2 + q3): results depend on (N, K, nsplit).
+// (At M = 128 this form is slower than k_gemm_ws: its 8 activation fragments per k-step are
+// 16-row gathers -- DESIGN.md "rejected designs".)
+template <int MODE, int NTW, int KS, int PF>
+__global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A, long lda,
+                                                    const bf16_t* __restrict__ W, int M, int N, int K, int kslice,
+                                                    float* __restrict__ Cpart, bf16_t* __restrict__ Cout,
+                                                    const int32_t* skip) {
+    __shared__ __attribute__((aligned(16))) f32x4 red[4][NTW][64];
+    if (skip && *skip) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ln = lane & 15, lg = lane >> 4;
+    const int split = blockIdx.z;
+    const int nt0 = blockIdx.x * NTW;                          // first 16-column tile
+    const int ntiles = (N + 63) / 64 * 4;                      // packed rows are padded to 64
+    const int kbeg = split * kslice + w * (kslice >> 2);
+    const bf16_t* wp[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+        wp[t] = W + ((size_t)min(nt0 + t, ntiles - 1) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
+    const bf16_t* ap = A + (size_t)min(ln, M - 1) * lda + kbeg + lg * 8;
+    f32x4 acc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = PF + 1;
+    uint4 wr[U][NTW], ar[U];
+    auto issue = [&](int st, int slot) {
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) wr[slot][t] = ldg_w<true>(wp[t] + st * 512);
+        ar[slot] = *reinterpret_cast<const uint4*>(ap + st * 32);
+    };
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (p < KS) issue(p, p);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+        if (st + PF < KS) issue(st + PF, (st + PF) % U);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(ar[st % U]), as_frag(wr[st % U][t]), acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) red[w][t][lane] = acc[t];
+    __syncthreads();
+    // wave w finishes tiles t with t % 4 == w (NTW <= 4: one tile per wave at most)
+    const int t = w;
+    if (t >= NTW) return;
+    f32x4 sum = red[0][t][lane];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+        const f32x4 o = red[q][t][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sum[i] = sum[i] + o[i];
+    }
+    const int n = (nt0 + t) * 16 + ln;
+    if (MODE == 0) {
+        if (n < N) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = lg * 4 + i;
+                if (m < M) Cpart[(size_t)split * M * N + (size_t)m * N + n] = sum[i];
+            }
+        }
+    } else {
+        const int F = N / 2;
+        const int f = (nt0 + t) * 8 + (ln & 7);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float mine = round_bf(sum[i]);
+            const float other = __shfl_xor(mine, 8, 64);
+            const int m = lg * 4 + i;
+            if (ln < 8 && m < M && f < F) {
+                const float sl = round_bf(other / (1.0f + expf(-other)));
+                Cout[(size_t)m * F + f] = f2bf(mine * sl);
+            }
+        }
+    }
+}
+
 // nn.Linear [N][K] -> fragment-packed [Npad/16][K/32][64][8] (rows >= N zero)
 __global__ void k_pack_w(const bf16_t* __restrict__ w, int N, int K, int Npad, bf16_t* __restrict__ out) {
     const size_t total = (size_t)Npad / 16 * (K / 32) * 64;      // 16-byte pieces
@@ -553,6 +642,15 @@ __global__ void k_permute_fc1(const bf16_t* w, int F, int D, bf16_t* out) {
     for (int i = threadIdx.x; i < D / 8; i += blockDim.x) d[i] = s[i];
 }
 
+// ZK_GEMV=0 disables the small-M weight-stream GEMV (A/B tuning knob, read once)
+bool gemv_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ZK_GEMV");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 }  // namespace
 
 extern "C" int zk_pack_weights(const void* w, int N, int K, void* out, void* stream) {
@@ -573,6 +671,42 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemm_bf16: lda=%ld", lda);
     ZK_REQUIRE(mode == 0 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_bf16: bad mode/nsplit");
     const int nchunks = K / nsplit / BK;
+    if (M <= 16 && gemv_enabled() && (K / nsplit) % 128 == 0) {
+        // weight-stream GEMV (B <= 8 decode): 2 column tiles per workgroup, K quarters per wave
+        const int ks = K / nsplit / 128;
+        dim3 g((N + 31) / 32, 1, nsplit);
+        bool handled = false;
+#define ZK_GV(MODE_, KS_)                                                                                         \
+    do {                                                                                                          \
+        constexpr int PF_ = KS_ < 8 ? KS_ : 8;                                                                    \
+        hipLaunchKernelGGL((k_gemv_rk<MODE_, 2, KS_, PF_>), g, dim3(256), 0, (hipStream_t)stream,                 \
+                           (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,     \
+                           skip_flag);                                                                             \
+        handled = true;                                                                                           \
+    } while (0)
+        if (mode == 0) {
+            switch (ks) {
+                case 1: ZK_GV(0, 1); break;
+                case 2: ZK_GV(0, 2); break;
+                case 4: ZK_GV(0, 4); break;
+                case 8: ZK_GV(0, 8); break;
+                case 16: ZK_GV(0, 16); break;
+                default: break;
+            }
+        } else {
+            switch (ks) {
+                case 4: ZK_GV(1, 4); break;
+                case 8: ZK_GV(1, 8); break;
+                case 16: ZK_GV(1, 16); break;
+                default: break;
+            }
+        }
+#undef ZK_GV
+        if (handled) {
+            ZK_CHECK_LAUNCH("zk_gemm_bf16");
+            return 0;
+        }
+    }
 #ifndef ZK_WS2_MIN_CHUNKS
 #define ZK_WS2_MIN_CHUNKS 1000000
 #endif
