@@ -58,6 +58,24 @@ def gemm():
         del Ws
 
 
+def ln():
+    R, D = 128, 2048
+    for ns in (1, 4, 8):
+        ncopy = 16
+        parts = [torch.randn(ns * R * D, device=dev) for _ in range(ncopy)]
+        x = torch.randn(R, D, device=dev).to(torch.bfloat16)
+        w = torch.randn(D, device=dev).to(torch.bfloat16)
+        b = torch.randn(D, device=dev).to(torch.bfloat16)
+        xn = torch.empty_like(x)
+        it = [0]
+
+        def f():
+            p = parts[it[0] % ncopy]
+            it[0] += 1
+            call("zk_resid_ln", ptr(p), ns, ptr(x), ptr(w), ptr(b), 1e-5, R, D, ptr(x), ptr(xn), 0, None, S)
+        print(f"resid_ln rows={R} D={D} slabs={ns}: {timeit(f):6.2f} us", flush=True)
+
+
 def attn():
     R, H, Hk, hd = 128, 16, 4, 128
     for ctx in (512, 1705, 2999):
@@ -128,6 +146,8 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
         gemm()
+    if what in ("ln", "all"):
+        ln()
     if what in ("attn", "all"):
         attn()
     if what in ("dac", "all"):
