@@ -94,10 +94,11 @@ __global__ __launch_bounds__(LN_NT) void k_embed_ln(const int64_t* ids, int B, i
     float x[N8 * 8];
     // all code ids, then all embedding rows, issued before the first add (two memory round
     // trips per step instead of 2K dependent ones); K <= EMB_MAXK (host-checked)
+    // (loads unconditional with a clamped codebook index, so the arrays stay in registers)
     int64_t idv[EMB_MAXK];
 #pragma unroll
     for (int k = 0; k < EMB_MAXK; ++k) {
-        int64_t id = k < K ? ids[b * bstr + k * kstr + col] : 0;
+        const int64_t id = ids[b * bstr + min(k, K - 1) * kstr + col];
         idv[k] = id < 0 ? 0 : (id >= V ? V - 1 : id);
     }
 #pragma unroll
@@ -108,14 +109,14 @@ __global__ __launch_bounds__(LN_NT) void k_embed_ln(const int64_t* ids, int B, i
         uint4 ev[EMB_MAXK];
 #pragma unroll
         for (int k = 0; k < EMB_MAXK; ++k)
-            if (k < K) ev[k] = *reinterpret_cast<const uint4*>(emb + ((size_t)k * V + idv[k]) * D + c);
+            ev[k] = *reinterpret_cast<const uint4*>(emb + ((size_t)min(k, K - 1) * V + idv[k]) * D + c);
 #pragma unroll
         for (int k = 0; k < EMB_MAXK; ++k) {
-            if (k >= K) break;
             float e[8];
             unpack8(ev[k], e);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc[q] = (k == 0) ? e[q] : round_bf(acc[q] + e[q]);
+            for (int q = 0; q < 8; ++q)
+                if (k < K) acc[q] = (k == 0) ? e[q] : round_bf(acc[q] + e[q]);
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) x[j * 8 + q] = acc[q];

@@ -85,7 +85,7 @@ constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 // (it cannot tell the DMA's LDS range) costs nothing -- they have no loads in flight.
 // Step i = (chunk c, tap t); the loader runs CL_DA steps ahead for weights and DX steps
 // ahead for windows (DX >= CL_DA, window ring of NX slots), one raw s_barrier per step.
-template <int FM>
+template <int FM, bool SF32>
 __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
@@ -234,7 +234,10 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
             }
             if (xout) *reinterpret_cast<float4*>(xout + o) = make_float4(v0, v1, v2, v3);
             if (!sout) continue;
-            if (s_f32)      // fp32 Snake output for the fp32 tail (exact sinf, reference formula)
+            // fp32 Snake output for the fp32 tail (exact sinf, reference formula); a separate
+            // instantiation so the common epilogue stays small enough to unroll fully (the
+            // accumulators then never leave registers)
+            if (SF32)
                 reinterpret_cast<float4*>(sout)[o >> 2] =
                     make_float4(snake(v0, aa.x), snake(v1, aa.y), snake(v2, aa.z), snake(v3, aa.w));
             else
@@ -423,10 +426,10 @@ void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Ci
                  long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
                  int out_stride, int out_off0, int Tout, const float* resid, float* xout, const float* alpha,
                  void* sout, int s_f32, const int32_t* lens, int in_scale, int out_scale, int nq, int nx, int dx) {
+    auto kern = s_f32 ? &k_conv_cl<FM, true> : &k_conv_cl<FM, false>;
     if (lds > 65536)
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv_cl<FM>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
-    hipLaunchKernelGGL((k_conv_cl<FM>), dim3(nwg), dim3(CL_THREADS), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(CL_THREADS), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
                        dil, pad, Qn, nphase, out_stride, out_off0, Tout, resid, xout, alpha, sout, s_f32, lens,
                        in_scale, out_scale, nq, nx, dx);
 }
