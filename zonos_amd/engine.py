@@ -165,7 +165,10 @@ class HipDecoder:
         f32, bf, i32 = torch.float32, torch.bfloat16, torch.int32
         # heads: no split-K (145 workgroups of 64 columns stream 37.8 MB in 15.6 us vs 19.8 us
         # with 2 splits, tools/microbench.py gemm; the sampler then reads one slab)
-        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R), fc2=_split_for(D, Fd, R), heads=1)
+        # out_proj: 4-way split-K (128 workgroups) is as fast as 8-way (6.6 vs 6.5 us) and halves
+        # the fp32 slabs it writes and k_resid_ln reads (4.2 vs 8.4 MB; resid_ln 4.3 vs 4.8 us)
+        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R, target_blocks=128),
+                      fc2=_split_for(D, Fd, R), heads=1)
         splits.update(_split_overrides())
         part_n = max(Mp * Nqkv, Mp * D, splits["qkv"] * R * Nqkv, splits["o"] * R * D, splits["fc2"] * R * D,
                      splits["heads"] * R * Nh)
