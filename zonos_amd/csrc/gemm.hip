@@ -211,10 +211,7 @@ constexpr int WS_THREADS = 256 + 64 * WS_NLD;
 #ifndef ZK_WS_NT
 #define ZK_WS_NT 1
 #endif
-#ifndef ZK_WS_LDSPF
-#define ZK_WS_LDSPF 1
-#endif
-constexpr int WS_LDSPF = ZK_WS_LDSPF;   // chunks published ahead of the one being multiplied
+constexpr int WS_LDSPF = 1;      // chunks published ahead of the one being multiplied
 constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 
@@ -264,7 +261,7 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         const int pre = min(WS_DA, nchunks);
         for (int c = 0; c < pre; ++c) issue(c);
         for (int c = 0; c < nchunks; ++c) {
-            // barrier c publishes chunk `need` (ZK_WS_LDSPF: one chunk ahead, so the compute
+            // barrier c publishes chunk `need` (one chunk ahead, so the compute
             // waves can read chunk c+1's fragments while they multiply chunk c)
             const int need = min(c + WS_LDSPF, nchunks - 1);
             const int younger = min(c - 1 + WS_DA, nchunks - 1) - need;   // chunks issued after `need`
@@ -297,7 +294,6 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         wr0[p] = ldg_w<WS_NT>(wrow + pc * WCH);
         wr1[p] = ldg_w<WS_NT>(wrow + pc * WCH + WHALF);
     }
-#if ZK_WS_LDSPF
     // activation fragments of the next chunk are read from LDS (register double buffer) while
     // the current chunk is multiplied: the LDS latency after each barrier is off the MFMA path
     uint4 af[2][2][MT];
@@ -332,36 +328,6 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
                 acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(af[ch & 1][ks][mt]), b, acc[mt], 0, 0, 0);
         }
     }
-#else
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-        if (ch + PF < NCH) {
-            wr0[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH);
-            wr1[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH + WHALF);
-        }
-        __builtin_amdgcn_s_barrier();                               // chunk ch is in LDS
-        asm volatile("" ::: "memory");
-        const char* base = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-#ifndef ZK_DBG_NOMFMA
-                const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
-#else
-                if (mt == 0) {
-                    const uint4 rw = ks == 0 ? wr0[ch % U] : wr1[ch % U];
-                    acc[0][0] += __uint_as_float(rw.x ^ rw.w);
-                }
-                (void)base;
-                (void)b;
-#endif
-            }
-        }
-    }
-#endif
     if (MODE == 0) {
         float* C = Cpart + (size_t)split * M * N;
         if (wvalid) {
@@ -376,145 +342,6 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
     } else {
         const int F = N / 2;
         const int f = (n0 + w * 16) / 2 + (ln & 7);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float mine = round_bf(acc[mt][i]);
-                const float other = __shfl_xor(mine, 8, 64);
-                const int m = mt * 16 + lg * 4 + i;
-                if (ln < 8 && m < M && f < F) {
-                    const float sl = round_bf(other / (1.0f + expf(-other)));
-                    Cout[(size_t)m * F + f] = f2bf(mine * sl);
-                }
-            }
-    }
-}
-
-// ------------------------------------------------------------------ decode GEMM, two K halves per workgroup
-// Same tile (all M rows x 64 columns) and the same loader-wave activation ring as k_gemm_ws, but
-// 8 compute waves: waves 0-3 stream the first half of K for the tile's four 16-column groups,
-// waves 4-7 the second half. Twice the weight bytes in flight per CU at the same per-wave
-// prefetch depth (the once-read weight stream is latency-bound at one wave per SIMD), and no
-// extra HBM or partial-slab traffic: the halves are summed through LDS at the end (upper half
-// first, fixed order -> results independent of M). Ring slot = two 16-row-tile chunks (one per half).
-#ifndef ZK_WS2_NB
-#define ZK_WS2_NB 4
-#define ZK_WS2_DA 2
-#endif
-constexpr int WS2_NB = ZK_WS2_NB;
-constexpr int WS2_DA = ZK_WS2_DA;
-constexpr int WS2_THREADS = 576;
-
-template <int MODE, int NCHH, int PF, int MT>
-__global__ __launch_bounds__(WS2_THREADS, 1) void k_gemm_ws2(const bf16_t* __restrict__ A, long lda,
-                                                          const bf16_t* __restrict__ W, int M, int N, int K,
-                                                          int kslice, float* __restrict__ Cpart,
-                                                          bf16_t* __restrict__ Cout, const int32_t* skip) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (skip && *skip) return;
-    constexpr int TILE = MT * 16 * BK * 2;            // bytes of one half's chunk
-    const int n0 = blockIdx.x * BN, split = blockIdx.z;
-    const int kbeg = split * kslice;
-    const int khalf_len = kslice / 2;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int ln = lane & 15, lg = lane >> 4;
-
-    if (w == 8) {
-        constexpr int NP = 2 * MT;
-        const int rl = lane >> 3, sl = lane & 7;
-        auto issue = [&](int ch) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                char* dst = smem + (ch % WS2_NB) * (2 * TILE) + h * TILE;
-                const int k0 = kbeg + h * khalf_len + ch * BK;
-#pragma unroll
-                for (int i = 0; i < NP; ++i) {
-                    const int row = 8 * i + rl;
-                    const int m = min(row, M - 1);
-                    const bf16_t* src = A + (size_t)m * lda + k0 + ((sl ^ (row & 7)) << 3);
-                    __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 1024), 16, 0, 0);
-                }
-            }
-        };
-        const int pre = min(WS2_DA, NCHH);
-        for (int c = 0; c < pre; ++c) issue(c);
-        for (int c = 0; c < NCHH; ++c) {
-            static_assert(WS2_DA <= 2, "vmcnt holds at most 63 outstanding loads");
-            const int younger = min(c + WS2_DA, NCHH) - c - 1;
-            if (younger == 1) vm_wait<2 * NP>();
-            else vm_wait<0>();
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (c + WS2_DA < NCHH) issue(c + WS2_DA);
-        }
-        __syncthreads();                                  // the reduction's two barriers
-        __syncthreads();
-        return;
-    }
-
-    const int cg = w & 3, kh = w >> 2;
-    const int wn = n0 + cg * 16 + ln;
-    const bool wvalid = wn < N;
-    const bf16_t* wrow = w_base(W, n0 + cg * 16, wvalid ? wn : 0, K, kbeg + kh * khalf_len, lane);
-    f32x4 acc[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    constexpr int U = PF + 1;
-    uint4 wr0[U], wr1[U];
-#pragma unroll
-    for (int p = 0; p < PF; ++p) {
-        const int pc = p < NCHH ? p : NCHH - 1;
-        wr0[p] = ldg_w<WS_NT>(wrow + pc * WCH);
-        wr1[p] = ldg_w<WS_NT>(wrow + pc * WCH + WHALF);
-    }
-#pragma unroll
-    for (int ch = 0; ch < NCHH; ++ch) {
-        if (ch + PF < NCHH) {
-            wr0[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH);
-            wr1[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH + WHALF);
-        }
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const char* base = smem + (ch % WS2_NB) * (2 * TILE) + kh * TILE;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
-            }
-        }
-    }
-    // sum the halves: upper half parks its accumulators in LDS (the ring is free after the loop)
-    __syncthreads();
-    f32x4* red = reinterpret_cast<f32x4*>(smem) + (size_t)cg * MT * 64;
-    if (kh == 1) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) red[mt * 64 + lane] = acc[mt];
-    }
-    __syncthreads();
-    if (kh == 1) return;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const f32x4 o = red[mt * 64 + lane];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[mt][i] = acc[mt][i] + o[i];
-    }
-    if (MODE == 0) {
-        if (wvalid) {
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int m = mt * 16 + lg * 4 + i;
-                    if (m < M) Cpart[(size_t)split * M * N + (size_t)m * N + wn] = acc[mt][i];
-                }
-        }
-    } else {
-        const int F = N / 2;
-        const int f = (n0 + cg * 16) / 2 + (ln & 7);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -702,52 +529,6 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
             }
         }
 #undef ZK_GV
-        if (handled) {
-            ZK_CHECK_LAUNCH("zk_gemm_bf16");
-            return 0;
-        }
-    }
-#ifndef ZK_WS2_MIN_CHUNKS
-#define ZK_WS2_MIN_CHUNKS 1000000
-#endif
-    if (M <= BM && nchunks >= ZK_WS2_MIN_CHUNKS && nchunks <= 128 && nchunks % 2 == 0) {
-        const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
-        const size_t lds = std::max<size_t>((size_t)WS2_NB * 2 * MT * 16 * BK * 2, (size_t)4 * MT * 64 * 16);
-        dim3 g((N + BN - 1) / BN, 1, nsplit);
-        bool handled = false;
-#define ZK_WS2_LAUNCH3(MODE_, NCHH_, MT_)                                                                          \
-    do {                                                                                                          \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws2<MODE_, NCHH_, WS_PF, MT_>),          \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                \
-        hipLaunchKernelGGL((k_gemm_ws2<MODE_, NCHH_, WS_PF, MT_>), g, dim3(WS2_THREADS), lds, (hipStream_t)stream, \
-                           (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,     \
-                           skip_flag);                                                                             \
-        handled = true;                                                                                           \
-    } while (0)
-#define ZK_WS2_LAUNCH(MODE_, NCHH_)                                                                                \
-    do {                                                                                                          \
-        switch (MT) {                                                                                             \
-            case 1: ZK_WS2_LAUNCH3(MODE_, NCHH_, 1); break;                                                       \
-            case 2: ZK_WS2_LAUNCH3(MODE_, NCHH_, 2); break;                                                       \
-            case 4: ZK_WS2_LAUNCH3(MODE_, NCHH_, 4); break;                                                       \
-            default: ZK_WS2_LAUNCH3(MODE_, NCHH_, 8); break;                                                      \
-        }                                                                                                         \
-    } while (0)
-        if (mode == 0) {
-            switch (nchunks / 2) {
-                case 4: ZK_WS2_LAUNCH(0, 4); break;
-                case 8: ZK_WS2_LAUNCH(0, 8); break;
-                case 16: ZK_WS2_LAUNCH(0, 16); break;
-                default: break;
-            }
-        } else {
-            switch (nchunks / 2) {
-                case 16: ZK_WS2_LAUNCH(1, 16); break;
-                default: break;
-            }
-        }
-#undef ZK_WS2_LAUNCH3
-#undef ZK_WS2_LAUNCH
         if (handled) {
             ZK_CHECK_LAUNCH("zk_gemm_bf16");
             return 0;
