@@ -92,8 +92,15 @@ def _split_overrides() -> dict:
 def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> int:
     """Workgroups per (row, kv head) for flash-decoding. Measured at R=128 (B=64): one
     workgroup per (row, kv head) (512 workgroups, no combine pass) reads 5.4-5.7 TB/s at
-    ctx 1.7-3k vs 4.5-4.7 with 2 splits; small batches split the keys to fill the CUs."""
-    return max(1, min(-(-target_blocks // (R * Hkv)), smax // 128))
+    ctx 1.7-3k vs 4.5-4.7 with 2 splits. Small batches split the keys to fill the CUs, but
+    each split must cover >= 2048 keys of the cache: the combine launch costs ~6 us, more than
+    it saves below that (B=1, 10 s: 1.294 ms per decode step unsplit vs 1.353 with 10 splits,
+    tools/c2_attn_ab.sh)."""
+    if os.environ.get("ZK_ATTN_SPLITS"):          # tuning knob (not used by default)
+        return max(1, min(int(os.environ["ZK_ATTN_SPLITS"]), smax // 128))
+    want = -(-target_blocks // (R * Hkv))
+    cap = max(1, -(-smax // 2048))
+    return max(1, min(want, cap, smax // 128))
 
 
 class HipDecoder:
