@@ -59,6 +59,19 @@ def test_split_selection_batch_invariant():
         assert ((N + 63) // 64) * s >= 128
 
 
+def test_attention_split_rule():
+    """Flash-decoding key splits: none at B=64 (512 workgroups already), and each split covers
+    >= 2048 cached keys (a combine launch costs more than it saves below that)."""
+    from zonos_amd.engine import attn_splits_for
+    assert attn_splits_for(128, 4, 3072) == 1           # c3
+    assert attn_splits_for(2, 4, 1280) == 1             # c2: B=1, 10 s
+    assert attn_splits_for(2, 4, 3328) == 2             # B=1, 30 s
+    for R in (2, 8, 16, 64, 128):
+        for smax in (256, 1024, 3072, 8192):
+            s = attn_splits_for(R, 4, smax)
+            assert 1 <= s <= max(1, smax // 128) and (s == 1 or smax / s >= 1024)
+
+
 def test_kv_layout_pack_roundtrip():
     """zonos_amd.kvlayout (host view of backbone.hip k_off / v_off): pack/unpack are inverse
     and element positions follow the documented fragment order."""
