@@ -4,13 +4,17 @@
 // Shape of the work: the decode step multiplies 2B = 128 activation rows by weight
 // matrices streamed once from HBM (3.2 GB of weights per step), so the
 // tile is 128 rows x 64 columns: every row of the batch lives in one workgroup and each
-// weight element is read exactly once per step. 4 waves; wave w owns 16 weight rows
-// (output columns) and all 128 activation rows, so its B fragments come straight from
-// HBM into registers (no LDS round trip for the once-read stream) while the activation
-// tile -- re-read by every column tile, L2-resident -- is staged in LDS (XOR-swizzled,
-// double-buffered, 64-deep K chunks). Split-K over gridDim.z fills the 256 CUs when N is
-// small; the partial slabs are reduced by the consumer kernel (k_resid_ln / k_qkv_rope /
-// the sampler), in a fixed order, so results do not depend on M (batch-invariant).
+// weight element is read exactly once per step. Three kernels:
+//   k_gemm     (M > 128: prefill) 4 waves, activation tile staged in LDS by the waves themselves;
+//   k_gemm_ws  (16 < M <= 128: decode) 4 compute waves stream the weights into registers, 4
+//              loader waves move the activation chunks into LDS by LDS-DMA;
+//   k_gemv_rk  (M <= 16: small-batch decode) pure register weight stream, K quarters per wave.
+// Wave w of a 64-column tile owns 16 weight rows (output columns), so its B fragments come
+// straight from HBM into registers (no LDS round trip for the once-read stream) while the
+// activation tile -- re-read by every column tile, L2-resident -- comes from LDS. Split-K over
+// gridDim.z fills the 256 CUs when N is small; the partial slabs are reduced by the consumer
+// kernel (k_resid_ln / the attention prologue / the sampler) in a fixed order, so the results
+// depend on (N, K, nsplit) and the kernel regime, not on M within a regime.
 //
 // mode 0: fp32 partial slabs; mode 1: fused SwiGLU for FeedForward.fc1 (_torch.py:150-152).
 #include "common.h"

@@ -3,7 +3,7 @@
 SURVEY.md §8(e): utterances are independent, so the batch is split into contiguous blocks
 per rank (each rank keeps its own cond+uncond row pairs); the engine's noise stream is keyed
 by the global utterance index (row_base), so the codes equal a single-GPU batch. The only
-collective is one all_gather of the int16 codes + lengths at the end (RCCL over xGMI on the
+collective is one all_gather of the int32 codes + lengths at the end (RCCL over xGMI on the
 GPU box, gloo in the CPU tests)."""
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ def shard(global_batch: int, world: int, rank: int) -> tuple[int, int]:
 
 def gather_codes(codes: list, device=None, group=None) -> list:
     """All-gather a list of int [9, T_i] code tensors from every rank (rank order = global
-    utterance order). Codes travel as int16 (values <= 1025) padded to the max length."""
+    utterance order). Codes travel as int32 (values <= 1025) padded to the max length."""
     world = dist.get_world_size(group)
     device = device or (codes[0].device if codes else torch.device("cpu"))
     n = torch.tensor([len(codes)], device=device)
