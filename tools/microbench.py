@@ -58,6 +58,24 @@ def gemm():
         del Ws
 
 
+def prefill():
+    """Prefill GEMMs at c3 (M = 2B x (Lc + P + 1) = 128 x 411 rows, split-K 1)."""
+    M = 128 * 411
+    for name, N, K, mode in (("qkv", 3072, 2048, 0), ("o", 2048, 2048, 0), ("fc1", 16384, 2048, 1),
+                             ("fc2", 2048, 8192, 0)):
+        Wp = torch.randn((N + 63) // 64 * 64, K, device=dev).to(torch.bfloat16)
+        A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        part = torch.empty(M * N if mode == 0 else 1, device=dev)
+        out = torch.empty(M, N // 2 if mode == 1 else 1, dtype=torch.bfloat16, device=dev)
+
+        def f():
+            call("zk_gemm_bf16", ptr(A), K, ptr(Wp), M, N, K, 1, mode, ptr(part), ptr(out), None, S)
+        us = timeit(f, reps=10, warm=2)
+        print(f"prefill {name:4s} M={M} N={N:5d} K={K:5d}: {us / 1e3:7.3f} ms  "
+              f"{2.0 * M * N * K / (us * 1e-6) / 1e12:7.1f} TFLOP/s", flush=True)
+        del Wp, A, part, out
+
+
 def ln():
     R, D = 128, 2048
     for ns in (1, 4, 8):
@@ -146,6 +164,8 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
         gemm()
+    if what in ("prefill", "all"):
+        prefill()
     if what in ("ln", "all"):
         ln()
     if what in ("attn", "all"):

@@ -64,22 +64,32 @@ ZK_DEV const bf16_t* w_base(const bf16_t* W, int, int row, int K, int kbeg, int 
 // LDS byte offset of 16-byte chunk c (0..7) of tile row `row` (128-byte rows, XOR swizzle)
 ZK_DEV int lds_off(int row, int c) { return row * 128 + ((c ^ (row & 7)) << 4); }
 
-template <int MODE, int U, bool WNT = false>
+// NTW 16-column tiles per wave (tile 128 x 64*NTW): every activation fragment read from LDS
+// feeds NTW MFMAs -- with NTW = 1 the four waves' fragment reads (1 KB per MFMA each) exceed the
+// LDS array's 256 B/clk, with NTW = 2 the prefill GEMMs become MFMA-bound.
+template <int MODE, int U, bool WNT = false, int NTW = 1>
 __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ W,
                                              int M, int N, int K, int kslice, float* __restrict__ Cpart,
                                              bf16_t* __restrict__ Cout, const int32_t* skip) {
     __shared__ __attribute__((aligned(16))) char smem[2 * BM * BK * 2];
     if (skip && *skip) return;
-    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, split = blockIdx.z;
+    const int n0 = blockIdx.x * BN * NTW, m0 = blockIdx.y * BM, split = blockIdx.z;
     const int kbeg = split * kslice;
     const int nchunks = kslice / BK;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int ln = lane & 15, lg = lane >> 4;
 
-    // this lane's weight row
-    const int wn = n0 + w * 16 + ln;
-    const bool wvalid = wn < N;
-    const bf16_t* wrow = w_base(W, n0 + w * 16, wvalid ? wn : 0, K, kbeg, lane);
+    // this lane's weight rows (one per 16-column tile of the wave)
+    int wn[NTW];
+    bool wvalid[NTW];
+    const bf16_t* wrow[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+        const int c0 = n0 + (w * NTW + t) * 16;
+        wn[t] = c0 + ln;
+        wvalid[t] = wn[t] < N;
+        wrow[t] = w_base(W, c0, wvalid[t] ? wn[t] : 0, K, kbeg, lane);
+    }
 
     // activation staging: 4 x 16 B per thread per K chunk (row = q>>3, 16-B chunk = q&7)
     const bf16_t* arow[4];
@@ -109,23 +119,28 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
         *reinterpret_cast<uint4*>(_b + aoff[3]) = a3;                         \
     } while (0)
 
-    f32x4 acc[8];
+    f32x4 acc[8][NTW];
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // Weight stream: a register ring of U chunk slots keeps U-1 chunks (2 KB per wave each)
-    // of the once-read weights in flight while the current chunk is multiplied. Every load
-    // is unconditional (indices clamped; invalid columns stream row 0 and are never stored)
-    // so hipcc emits counted vmcnt waits, and the activation loads of the next chunk are
-    // issued BEFORE the weight prefetch so the wait that retires them (vmcnt counts in issue
-    // order) leaves the weight loads in flight. nchunks % U == 0 (host-checked).
+    // Weight stream: a register ring of U chunk slots keeps U-1 chunks (2 KB per wave and tile
+    // each) of the weights in flight while the current chunk is multiplied. Every load is
+    // unconditional (indices clamped; invalid columns stream row 0 and are never stored) so
+    // hipcc emits counted vmcnt waits, and the activation loads of the next chunk are issued
+    // BEFORE the weight prefetch so the wait that retires them (vmcnt counts in issue order)
+    // leaves the weight loads in flight. nchunks % U == 0 (host-checked).
     constexpr int PF = U - 1;
-    uint4 wr0[U], wr1[U];
+    uint4 wr0[U][NTW], wr1[U][NTW];
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
         const int pc = min(p, nchunks - 1);
-        wr0[p] = ldg_w<WNT>(wrow + pc * WCH);
-        wr1[p] = ldg_w<WNT>(wrow + pc * WCH + WHALF);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+            wr0[p][t] = ldg_w<WNT>(wrow[t] + pc * WCH);
+            wr1[p][t] = ldg_w<WNT>(wrow[t] + pc * WCH + WHALF);
+        }
     }
     ZK_LOAD_A(0);
     ZK_STORE_A(0);
@@ -137,17 +152,22 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
             ZK_LOAD_A(min(ch + 1, nchunks - 1));
             {
                 const int pc = min(ch + PF, nchunks - 1);
-                wr0[(u + PF) % U] = ldg_w<WNT>(wrow + pc * WCH);
-                wr1[(u + PF) % U] = ldg_w<WNT>(wrow + pc * WCH + WHALF);
+#pragma unroll
+                for (int t = 0; t < NTW; ++t) {
+                    wr0[(u + PF) % U][t] = ldg_w<WNT>(wrow[t] + pc * WCH);
+                    wr1[(u + PF) % U][t] = ldg_w<WNT>(wrow[t] + pc * WCH + WHALF);
+                }
             }
             const char* base = smem + (ch & 1) * (BM * BK * 2);
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                const bf16x8 b = as_frag(ks == 0 ? wr0[u] : wr1[u]);
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) {
                     const uint4 a = *reinterpret_cast<const uint4*>(base + lds_off(mt * 16 + ln, ks * 4 + lg));
-                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), b, acc[mt], 0, 0, 0);
+#pragma unroll
+                    for (int t = 0; t < NTW; ++t)
+                        acc[mt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            as_frag(a), as_frag(ks == 0 ? wr0[u][t] : wr1[u][t]), acc[mt][t], 0, 0, 0);
                 }
             }
             ZK_STORE_A((ch + 1) & 1);
@@ -157,35 +177,38 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
 #undef ZK_LOAD_A
 #undef ZK_STORE_A
 
-    // epilogue: acc[mt][i] = C[m0 + 16mt + 4lg + i][wn]
-    if (MODE == 0) {
-        float* C = Cpart + (size_t)split * M * N;
-        if (wvalid) {
+    // epilogue: acc[mt][t][i] = C[m0 + 16mt + 4lg + i][wn[t]]
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+        if (MODE == 0) {
+            float* C = Cpart + (size_t)split * M * N;
+            if (wvalid[t]) {
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = m0 + mt * 16 + lg * 4 + i;
+                        if (m < M) C[(size_t)m * N + wn[t]] = acc[mt][t][i];
+                    }
+            }
+        } else {
+            // interleaved fc1 rows: within each group of 16 columns, 0..7 = y[f0..f0+7], 8..15 = gate[f0..]
+            const int F = N / 2;
+            const int f = (n0 + (w * NTW + t) * 16) / 2 + (ln & 7);
 #pragma unroll
             for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
+                    const float mine = round_bf(acc[mt][t][i]);
+                    const float other = __shfl_xor(mine, 8, 64);
                     const int m = m0 + mt * 16 + lg * 4 + i;
-                    if (m < M) C[(size_t)m * N + wn] = acc[mt][i];
+                    if (ln < 8 && m < M && f < F) {
+                        const float y = mine, g = other;
+                        const float sl = round_bf(g / (1.0f + expf(-g)));     // F.silu in bf16
+                        Cout[(size_t)m * F + f] = f2bf(y * sl);
+                    }
                 }
         }
-    } else {
-        // interleaved fc1 rows: within each group of 16 columns, 0..7 = y[f0..f0+7], 8..15 = gate[f0..]
-        const int F = N / 2;
-        const int f = (n0 + w * 16) / 2 + (ln & 7);
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float mine = round_bf(acc[mt][i]);
-                const float other = __shfl_xor(mine, 8, 64);
-                const int m = m0 + mt * 16 + lg * 4 + i;
-                if (ln < 8 && m < M && f < F) {
-                    const float y = mine, g = other;
-                    const float sl = round_bf(g / (1.0f + expf(-g)));     // F.silu in bf16
-                    Cout[(size_t)m * F + f] = f2bf(y * sl);
-                }
-            }
     }
 }
 
@@ -473,6 +496,15 @@ __global__ void k_permute_fc1(const bf16_t* w, int F, int D, bf16_t* out) {
     for (int i = threadIdx.x; i < D / 8; i += blockDim.x) d[i] = s[i];
 }
 
+// ZK_PREFILL_NTW=1 keeps one 16-column tile per wave in the large-M GEMM (A/B knob, read once)
+bool prefill_ntw2() {
+    static const bool on = [] {
+        const char* e = getenv("ZK_PREFILL_NTW");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
 // ZK_GEMV=0 disables the small-M weight-stream GEMV (A/B tuning knob, read once)
 bool gemv_enabled() {
     static const bool on = [] {
@@ -587,11 +619,22 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
 #undef ZK_WS_LAUNCH3
 #undef ZK_WS_LAUNCH
     }
-    dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, nsplit);
+    // large M (prefill): two 16-column tiles per wave for the slab GEMMs (c3 prefill: in_proj
+    // 1.01 vs 1.09 ms, fc2 1.98 vs 2.29 ms; the SwiGLU fc1 is faster with one: 4.87 vs 5.24 ms)
+    const int ntw = (prefill_ntw2() && mode == 0 && M > BM && N >= 8 * BN) ? 2 : 1;
+    dim3 grid((N + BN * ntw - 1) / (BN * ntw), (M + BM - 1) / BM, nsplit);
     const int U = (nchunks % 4 == 0) ? 4 : (nchunks % 2 == 0 ? 2 : 1);
 #define ZK_GEMM_LAUNCH(MODE_, U_)                                                                         \
-    hipLaunchKernelGGL((k_gemm<MODE_, U_>), grid, dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)A, lda, \
-                       (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout, skip_flag)
+    do {                                                                                                  \
+        if (ntw == 2)                                                                                     \
+            hipLaunchKernelGGL((k_gemm<MODE_, U_, false, 2>), grid, dim3(NT), 0, (hipStream_t)stream,     \
+                               (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart,       \
+                               (bf16_t*)Cout, skip_flag);                                                 \
+        else                                                                                              \
+            hipLaunchKernelGGL((k_gemm<MODE_, U_>), grid, dim3(NT), 0, (hipStream_t)stream,               \
+                               (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart,       \
+                               (bf16_t*)Cout, skip_flag);                                                 \
+    } while (0)
     if (mode == 0) {
         if (U == 4) ZK_GEMM_LAUNCH(0, 4); else if (U == 2) ZK_GEMM_LAUNCH(0, 2); else ZK_GEMM_LAUNCH(0, 1);
     } else {
