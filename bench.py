@@ -11,7 +11,7 @@ turns all codes into waveforms. One "step" = generate() + DAC decode of the whol
 batch.
 
 Multi-GPU: one process per GPU (torchrun), utterances sharded by rank (row_base keys the
-noise, so codes equal a single big batch), RCCL all_gather of the int16 codes at the end
+noise, so codes equal a single big batch), RCCL all_gather of the int32 codes at the end
 of each step; value = codes of all ranks / max-over-ranks wall time ("scaling": "weak").
 
 Prints ONE JSON line on rank 0.

@@ -77,9 +77,11 @@ def test_delay_pattern_golden():
 @pytest.mark.parametrize("M,N,K,nsplit", [(128, 3072, 2048, 8), (7, 1026 * 9, 256, 2), (300, 192, 512, 1),
                                           (128, 2048, 8192, 16), (2, 2048, 2048, 4), (20, 3072, 1024, 2),
                                           (64, 1168, 256, 4), (128, 3072, 2048, 1), (33, 1024, 8192, 1),
-                                          # k_gemm_rk shapes (decode, M <= 128): 4- and 2-tile workgroups
+                                          # decode shapes (k_gemm_ws / k_gemv_rk)
                                           (128, 2048, 2048, 8), (128, 9234, 2048, 2), (128, 16384, 2048, 1),
-                                          (128, 2048, 2048, 4), (100, 2048, 8192, 4), (1, 3072, 2048, 2)])
+                                          (128, 2048, 2048, 4), (100, 2048, 8192, 4), (1, 3072, 2048, 2),
+                                          # prefill shapes (k_gemm, M >= 1024)
+                                          (1100, 256, 512, 1), (2048, 384, 2048, 1), (1024, 1152, 128, 1)])
 def test_gemm_vs_fp32(M, N, K, nsplit):
     from zonos_amd._lib import call, ptr, stream_ptr
     g = torch.Generator(device="cpu").manual_seed(M + N)
@@ -113,7 +115,7 @@ def test_pack_weights_layout():
 
 
 @pytest.mark.parametrize("M,Fd,D", [(130, 256, 512), (2, 256, 512), (40, 256, 512), (128, 512, 2048),
-                                    (3, 512, 2048)])
+                                    (3, 512, 2048), (1030, 256, 512)])
 def test_gemm_swiglu(M, Fd, D):
     from zonos_amd._lib import call, ptr, stream_ptr
     g = torch.Generator(device="cpu").manual_seed(1)
