@@ -44,21 +44,36 @@ ZK_DEV size_t v_off(int key, int ch) {      // channel ch of key
 // ------------------------------------------------------------------ LayerNorm helper
 // Row of D elements, 8 per thread (D = 8 * NT * n8). Two-pass mean/var in fp32,
 // y = (x - mean) * rstd * w + b rounded to bf16 (nn.LayerNorm, eps from config).
+// wv / bv: this thread's 8-element chunks of w and b, loaded by the caller before its own
+// loads complete (so they share the row's memory round trip); red: 2 * NT / 64 floats (one
+// partial-sum slot per wave for the mean and one for the variance: one barrier per reduction).
 template <int NT, int n8>
-ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, int D, bf16_t* y,
-                   float* red) {
+ZK_DEV void ln_row_pre(const float* x, const uint4* wv, const uint4* bv, float eps, int D, bf16_t* y, float* red) {
+    const int w = threadIdx.x >> 6;
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < n8; ++j)
         if ((threadIdx.x + NT * j) * 8 < D)
             for (int e = 0; e < 8; ++e) s += x[j * 8 + e];
-    const float mean = block_sum<NT>(s, red) / (float)D;
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[w] = s;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    const float mean = t / (float)D;
     float v = 0.f;
 #pragma unroll
     for (int j = 0; j < n8; ++j)
         if ((threadIdx.x + NT * j) * 8 < D)
             for (int e = 0; e < 8; ++e) { const float d = x[j * 8 + e] - mean; v += d * d; }
-    const float var = block_sum<NT>(v, red) / (float)D;
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[NT / 64 + w] = v;
+    __syncthreads();
+    t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[NT / 64 + i];
+    const float var = t / (float)D;
     const float rstd = 1.0f / sqrtf(var + eps);
     const float nb = -rstd * mean;
 #pragma unroll
@@ -66,13 +81,29 @@ ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, 
         const int c = (threadIdx.x + NT * j) * 8;
         if (c >= D) continue;
         float wf[8], bf[8], o[8];
-        unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
-        unpack8(*reinterpret_cast<const uint4*>(b + c), bf);
+        unpack8(wv[j], wf);
+        unpack8(bv[j], bf);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
             o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(x[j * 8 + e], rstd), nb), wf[e]), bf[e]);
         *reinterpret_cast<uint4*>(y + c) = pack8(o);
     }
+}
+// the caller's w / b chunks (clamped index: unconditional loads stay in registers)
+template <int NT, int n8>
+ZK_DEV void ln_load_wb(const bf16_t* w, const bf16_t* b, int D, uint4* wv, uint4* bv) {
+#pragma unroll
+    for (int j = 0; j < n8; ++j) {
+        const int c = min((int)(threadIdx.x + NT * j) * 8, D - 8);
+        wv[j] = *reinterpret_cast<const uint4*>(w + c);
+        bv[j] = *reinterpret_cast<const uint4*>(b + c);
+    }
+}
+template <int NT, int n8>
+ZK_DEV void ln_row(const float* x, const bf16_t* w, const bf16_t* b, float eps, int D, bf16_t* y, float* red) {
+    uint4 wv[n8], bv[n8];
+    ln_load_wb<NT, n8>(w, b, D, wv, bv);
+    ln_row_pre<NT, n8>(x, wv, bv, eps, D, y, red);
 }
 
 constexpr int LN_NT = 256;
@@ -85,7 +116,7 @@ __global__ __launch_bounds__(LN_NT) void k_embed_ln(const int64_t* ids, int B, i
                                                     const int32_t* col_dev, int col_add, const bf16_t* emb, int V,
                                                     int D, bf16_t* x_out, int out_S, int out_t0, const bf16_t* lw,
                                                     const bf16_t* lb, float eps, bf16_t* xn_out, const int32_t* skip) {
-    __shared__ float red[LN_NT / 64];
+    __shared__ float red[2 * LN_NT / 64];
     if (skip && *skip) return;
     const int r = blockIdx.x / S, t = blockIdx.x % S, b = r % B;
     const int row = r * out_S + out_t0 + t;   // output row
@@ -128,7 +159,7 @@ __global__ __launch_bounds__(LN_NT) void k_embed_ln(const int64_t* ids, int B, i
 template <int N8>
 __global__ __launch_bounds__(LN_NT) void k_layernorm(const bf16_t* x, const bf16_t* w, const bf16_t* b, float eps,
                                                      int D, bf16_t* y) {
-    __shared__ float red[LN_NT / 64];
+    __shared__ float red[2 * LN_NT / 64];
     const int row = blockIdx.x;
     constexpr int n8 = N8;
     float xv[N8 * 8];
@@ -146,11 +177,17 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
                                                     const bf16_t* w, const bf16_t* b, float eps, int rows, int D,
                                                     bf16_t* x_out, bf16_t* xn_out, int ln_on_sum,
                                                     const int32_t* skip) {
-    __shared__ float red[LN_NT / 64];
+    __shared__ float red[2 * LN_NT / 64];
     if (skip && *skip) return;
     const int row = blockIdx.x;
     constexpr int n8 = N8;
     const size_t slab = (size_t)rows * D;
+    // LayerNorm weights and the residual row issued with the slab loads: one memory round trip
+    uint4 wv[N8], bv[N8], xiv[N8];
+    ln_load_wb<LN_NT, N8>(w, b, D, wv, bv);
+#pragma unroll
+    for (int j = 0; j < n8; ++j)
+        xiv[j] = *reinterpret_cast<const uint4*>(x_in + (size_t)row * D + min((int)(threadIdx.x + LN_NT * j) * 8, D - 8));
     float xv[N8 * 8];
 #pragma unroll
     for (int j = 0; j < n8; ++j) {
@@ -189,7 +226,7 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
             }
         }
         float xi[8];
-        unpack8(*reinterpret_cast<const uint4*>(x_in + (size_t)row * D + c), xi);
+        unpack8(xiv[j], xi);
         // transformer (_torch.py:100-101): x = bf16(x + bf16(proj)), LN of the rounded x;
         // ln_on_sum (mamba_ssm layer_norm_fn prenorm): LN of the fp32 sum, residual stored bf16
 #pragma unroll
@@ -200,7 +237,7 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
             for (int e = 0; e < 8; ++e) xv[j * 8 + e] = round_bf(xv[j * 8 + e]);
         }
     }
-    ln_row<LN_NT, N8>(xv, w, b, eps, D, xn_out + (size_t)row * D, red);
+    ln_row_pre<LN_NT, N8>(xv, wv, bv, eps, D, xn_out + (size_t)row * D, red);
 }
 
 // ------------------------------------------------------------------ in_proj epilogue
