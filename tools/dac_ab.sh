@@ -1,8 +1,9 @@
 #!/bin/bash
-# DAC per-layer timing, product vs lib/variants/* (GPU box)
+# DAC A/B: product vs zonos_amd/lib/variants/*: per-shape conv timing (tools/dac_layers.py), alternating
 set -e
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_dac_cl.py tests/test_gpu_dac.py tests/test_gpu_dac_enc.py 2>&1 | tail -1
-for v in product $(ls zonos_amd/lib/variants); do
-  lp=""; [ "$v" != product ] && lp=zonos_amd/lib/variants/$v/libzonos_hip.so
-  echo "== $v"; ZK_LIB_PATH=$lp timeout -k 10 300 python tools/dac_layers.py 16 2589 2>&1 | grep -v amdgpu
+for i in 1 2; do
+  echo "== product"; timeout -k 10 180 python tools/dac_layers.py 16 2589 2>&1 | grep -v amdgpu | head -8
+  for v in $(ls zonos_amd/lib/variants); do
+    echo "== $v"; ZK_LIB_PATH=zonos_amd/lib/variants/$v/libzonos_hip.so timeout -k 10 180 python tools/dac_layers.py 16 2589 2>&1 | grep -v amdgpu | head -8
+  done
 done

@@ -85,7 +85,7 @@ constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 // (it cannot tell the DMA's LDS range) costs nothing -- they have no loads in flight.
 // Step i = (chunk c, tap t); the loader runs CL_DA steps ahead for weights and DX steps
 // ahead for windows (DX >= CL_DA, window ring of NX slots), one raw s_barrier per step.
-template <int FM, bool SF32>
+template <int FM, bool SF32, bool RES>
 __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
@@ -182,6 +182,23 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
 #pragma unroll
         for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // RES (resid != nullptr: the 1x1 convs of the residual units): the residual tile is loaded
+    // before the main loop, so its latency overlaps the loader's first DMA instead of following
+    // the last MFMA (clamped, unconditional loads; out-of-range positions are never stored).
+    // A separate instantiation: the 64 extra registers would cost the k7 convs occupancy.
+    float4 rv[RES ? FM : 1][4];
+    if constexpr (RES) {
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int q = q0 + wn * 64 + n * 16 + ln;
+                const int tt = min(max(q * out_stride + out_off0 + phase, 0), Tout - 1);
+                rv[m][n] = *reinterpret_cast<const float4*>(
+                    resid + ((size_t)b * Tout + tt) * Cout + co0 + wm * 16 * FM + m * 16 + lg * 4);
+            }
+    }
+
     for (int s = 0; s < nstep; ++s) {
         const int c = s / ks, t = s - c * ks;
         __builtin_amdgcn_s_barrier();            // step s is in LDS
@@ -224,8 +241,8 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
                 v1 = __fadd_rn(acc[m][n][1], bb.y);
                 v2 = __fadd_rn(acc[m][n][2], bb.z);
                 v3 = __fadd_rn(acc[m][n][3], bb.w);
-                if (resid) {
-                    const float4 r = *reinterpret_cast<const float4*>(resid + o);
+                if constexpr (RES) {
+                    const float4 r = rv[m][n];
                     v0 = __fadd_rn(r.x, v0);
                     v1 = __fadd_rn(r.y, v1);
                     v2 = __fadd_rn(r.z, v2);
@@ -426,7 +443,8 @@ void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Ci
                  long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
                  int out_stride, int out_off0, int Tout, const float* resid, float* xout, const float* alpha,
                  void* sout, int s_f32, const int32_t* lens, int in_scale, int out_scale, int nq, int nx, int dx) {
-    auto kern = s_f32 ? &k_conv_cl<FM, true> : &k_conv_cl<FM, false>;
+    auto kern = resid ? (s_f32 ? &k_conv_cl<FM, true, true> : &k_conv_cl<FM, false, true>)
+                      : (s_f32 ? &k_conv_cl<FM, true, false> : &k_conv_cl<FM, false, false>);
     if (lds > 65536)
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(CL_THREADS), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
