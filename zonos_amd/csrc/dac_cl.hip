@@ -12,8 +12,9 @@
 // (modeling_dac.py:95-100 Snake, :222-233 residual unit, :266-278 decoder block, :420-439).
 //
 // Implicit GEMM on v_mfma_f32_16x16x32_f16: M = output channels, N = positions, K = (tap,
-// input channel). Workgroup tile CO_T = 32*FM channels x QT = 128 positions, 4 waves as 2x2,
-// each wave (16*FM) x 64. K is walked as steps (channel chunk c of CI, tap t): per chunk the
+// input channel). Workgroup tile CO_T = 32*FM channels x QT = 32*NQ positions (128, or 256 for
+// the convs without a residual: twice the positions per prologue / barrier / epilogue), 4 waves
+// as 2x2, each wave (16*FM) x (16*NQ). K is walked as steps (channel chunk c of CI, tap t): per chunk the
 // input window (QT + (ks-1)*dil positions x CI channels) is staged once and reused by all
 // taps (tap t reads rows shifted by t*dil); the (tap, chunk) weight slice is staged per step.
 // Both images land in LDS by LDS-DMA (global_load_lds_dwordx4, lane-linear destination, XOR
@@ -24,13 +25,14 @@
 #include "common.h"
 #include "../../include/zonos_hip.h"
 #include <algorithm>
+#include <stdlib.h>
 
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int QT = 128;          // positions per workgroup
+constexpr int QT = 128;          // positions per workgroup (NQ = 4)
 constexpr int MAXSPAN = 64;      // max (ks-1)*dil
 
 __device__ __attribute__((aligned(256))) uint4 g_zero_page[16];   // 256 zero bytes (LDS-DMA source for padding)
@@ -85,7 +87,7 @@ constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 // (it cannot tell the DMA's LDS range) costs nothing -- they have no loads in flight.
 // Step i = (chunk c, tap t); the loader runs CL_DA steps ahead for weights and DX steps
 // ahead for windows (DX >= CL_DA, window ring of NX slots), one raw s_barrier per step.
-template <int FM, bool SF32, bool RES>
+template <int FM, bool SF32, bool RES, int NQ>
 __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
@@ -107,10 +109,11 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
     const int L = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (id >> 3);
     const int cot = L % nco, qtile = (L / nco) % nq, b = L / (nco * nq);
     const int phase = cot % nphase, co0 = (cot / nphase) * CO_T;
-    const int q0 = qtile * QT;
+    constexpr int QTT = 32 * NQ;
+    const int q0 = qtile * QTT;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int win = QT + (ks - 1) * dil;
+    const int win = QTT + (ks - 1) * dil;
     const int nxp = (win + 15) >> 4;             // window pieces (16 rows each)
     const int XS = nxp * 1024;
     char* const wring = smem;
@@ -176,23 +179,23 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
 
     // ---------------- compute waves 0-3: 2 (co) x 2 (positions)
     const int ln = lane & 15, lg = lane >> 4, wm = wv >> 1, wn = wv & 1;
-    f32x4 acc[FM][4];
+    f32x4 acc[FM][NQ];
 #pragma unroll
     for (int m = 0; m < FM; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < NQ; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // RES (resid != nullptr: the 1x1 convs of the residual units): the residual tile is loaded
     // before the main loop, so its latency overlaps the loader's first DMA instead of following
     // the last MFMA (clamped, unconditional loads; out-of-range positions are never stored).
     // A separate instantiation: the 64 extra registers would cost the k7 convs occupancy.
-    float4 rv[RES ? FM : 1][4];
+    float4 rv[RES ? FM : 1][NQ];
     if constexpr (RES) {
 #pragma unroll
         for (int m = 0; m < FM; ++m)
 #pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const int q = q0 + wn * 64 + n * 16 + ln;
+            for (int n = 0; n < NQ; ++n) {
+                const int q = q0 + wn * 16 * NQ + n * 16 + ln;
                 const int tt = min(max(q * out_stride + out_off0 + phase, 0), Tout - 1);
                 rv[m][n] = *reinterpret_cast<const float4*>(
                     resid + ((size_t)b * Tout + tt) * Cout + co0 + wm * 16 * FM + m * 16 + lg * 4);
@@ -205,21 +208,21 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
         asm volatile("" ::: "memory");
         const char* xb = xring + (c % nx_slots) * XS;
         const char* wb = wring + (s % CL_NW) * WS;
-        uint4 a[FM], bq[4];
+        uint4 a[FM], bq[NQ];
 #pragma unroll
         for (int m = 0; m < FM; ++m)
             a[m] = *reinterpret_cast<const uint4*>(wb + I::off(wm * 16 * FM + m * 16 + ln, lg));
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-            bq[n] = *reinterpret_cast<const uint4*>(xb + I::off(wn * 64 + n * 16 + ln + t * dil, lg));
+        for (int n = 0; n < NQ; ++n)
+            bq[n] = *reinterpret_cast<const uint4*>(xb + I::off(wn * 16 * NQ + n * 16 + ln + t * dil, lg));
 #pragma unroll
         for (int m = 0; m < FM; ++m)
 #pragma unroll
-            for (int n = 0; n < 4; ++n)
+            for (int n = 0; n < NQ; ++n)
                 acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a[m]), as_h8(bq[n]), acc[m][n], 0, 0, 0);
     }
 
-    // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 64wn + 16n + ln]
+    // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 16NQ wn + 16n + ln]
     const int len_out = lens ? lens[b] * out_scale : Tout;
     const int out_off = out_off0 + phase;
 #pragma unroll
@@ -230,8 +233,8 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
         const float r0 = __fdiv_rn(1.0f, __fadd_rn(aa.x, 1e-9f)), r1 = __fdiv_rn(1.0f, __fadd_rn(aa.y, 1e-9f));
         const float r2 = __fdiv_rn(1.0f, __fadd_rn(aa.z, 1e-9f)), r3 = __fdiv_rn(1.0f, __fadd_rn(aa.w, 1e-9f));
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const int q = q0 + wn * 64 + n * 16 + ln;
+        for (int n = 0; n < NQ; ++n) {
+            const int q = q0 + wn * 16 * NQ + n * 16 + ln;
             const int tt = q * out_stride + out_off;
             if (q >= Qn || tt < 0 || tt >= Tout) continue;
             const size_t o = ((size_t)b * Tout + tt) * Cout + co;
@@ -438,13 +441,24 @@ __global__ __launch_bounds__(256) void k_rvq_encode(const float* __restrict__ z,
     }
 }
 
-template <int FM>
+// ZK_DAC_WIDE=0 keeps 128-position tiles everywhere (A/B knob, read once)
+bool dac_wide_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ZK_DAC_WIDE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+template <int FM, int NQ>
 void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Cin, int Tin, const uint16_t* w,
                  long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
                  int out_stride, int out_off0, int Tout, const float* resid, float* xout, const float* alpha,
                  void* sout, int s_f32, const int32_t* lens, int in_scale, int out_scale, int nq, int nx, int dx) {
-    auto kern = resid ? (s_f32 ? &k_conv_cl<FM, true, true> : &k_conv_cl<FM, false, true>)
-                      : (s_f32 ? &k_conv_cl<FM, true, false> : &k_conv_cl<FM, false, false>);
+    auto kern = &k_conv_cl<FM, false, false, NQ>;     // NQ = 8: fp16 output, no residual only
+    if constexpr (NQ == 4)
+        kern = resid ? (s_f32 ? &k_conv_cl<FM, true, true, NQ> : &k_conv_cl<FM, false, true, NQ>)
+                     : (s_f32 ? &k_conv_cl<FM, true, false, NQ> : kern);
     if (lds > 65536)
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(CL_THREADS), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
@@ -504,7 +518,13 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     if (B == 0 || Qn <= 0) return 0;
     const int nco = Cout / 32;
     const int FM = nco % 4 == 0 ? 4 : (nco % 3 == 0 ? 3 : (nco % 2 == 0 ? 2 : 1));
-    const int win = QT + (ks - 1) * dil;
+    // 256-position tiles for the plain convs without a residual at FM <= 3 (the 96-192-channel k7
+    // convs, overhead-bound at 128: -6 % / -15 %); the residual convs keep 128 (their prefetched
+    // residual tile would not fit the registers beside twice the accumulators), and so do the
+    // polyphase ConvTranspose convs (+12-22 % with 256, profiles/r1_dac_wide_tiles_ab.txt)
+    const bool wide = resid == nullptr && !s_f32 && nphase == 1 && FM <= 3 && dac_wide_enabled();
+    const int qt = wide ? 2 * QT : QT;
+    const int win = qt + (ks - 1) * dil;
     const size_t xs = (size_t)((win + 15) / 16) * 1024;
     const size_t ws = (size_t)32 * FM * 64;
     // window lead DX >= CL_DA steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
@@ -515,18 +535,19 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     }
     const size_t lds = CL_NW * ws + nx * xs;
     ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_conv_cl: LDS %zu too large", lds);
-    const int nq = (Qn + QT - 1) / QT;
+    const int nq = (Qn + qt - 1) / qt;
     const long nwg = (long)B * nq * (Cout / (32 * FM)) * nphase;
     ZK_REQUIRE(nwg < (1L << 31), "zk_dac_conv_cl: grid too large");
     hipStream_t st = (hipStream_t)stream;
-#define ZK_CL(F_)                                                                                           \
-    launch_conv<F_>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad, Qn, nphase, \
-                    out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32, lens, in_scale, out_scale, nq, nx, dx)
+#define ZK_CL(F_, NQ_)                                                                                           \
+    launch_conv<F_, NQ_>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad, Qn, nphase, \
+                         out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32, lens, in_scale, out_scale, nq, \
+                         nx, dx)
     switch (FM) {
-        case 4: ZK_CL(4); break;
-        case 3: ZK_CL(3); break;
-        case 2: ZK_CL(2); break;
-        default: ZK_CL(1); break;
+        case 4: ZK_CL(4, 4); break;
+        case 3: if (wide) ZK_CL(3, 8); else ZK_CL(3, 4); break;
+        case 2: if (wide) ZK_CL(2, 8); else ZK_CL(2, 4); break;
+        default: if (wide) ZK_CL(1, 8); else ZK_CL(1, 4); break;
     }
 #undef ZK_CL
     ZK_CHECK_LAUNCH("zk_dac_conv_cl");
