@@ -242,6 +242,15 @@ constexpr int WS_LDSPF = 1;      // chunks published ahead of the one being mult
 constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 
+// decode split-K slab stores (read once by the consumer kernel): non-temporal with ZK_SLAB_NT
+#ifndef ZK_SLAB_NT
+#define ZK_SLAB_NT 1
+#endif
+ZK_DEV void st_slab(float* p, float v) {
+    if constexpr (ZK_SLAB_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 template <int N_>
 ZK_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
 
@@ -363,7 +372,7 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int m = mt * 16 + lg * 4 + i;
-                    if (m < M) C[(size_t)m * N + wn] = acc[mt][i];
+                    if (m < M) st_slab(C + (size_t)m * N + wn, acc[mt][i]);
                 }
         }
     } else {
@@ -453,7 +462,7 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int m = lg * 4 + i;
-                if (m < M) Cpart[(size_t)split * M * N + (size_t)m * N + n] = sum[i];
+                if (m < M) st_slab(Cpart + (size_t)split * M * N + (size_t)m * N + n, sum[i]);
             }
         }
     } else {
