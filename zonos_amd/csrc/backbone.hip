@@ -315,6 +315,17 @@ struct KVFrag {
     uint4 v[8];      // [d-tile]
 };
 
+// KV cache slices: read once per step (hundreds of MB, beyond L2 and MALL), so with ZK_KV_NT
+// they are loaded non-temporally
+#ifndef ZK_KV_NT
+#define ZK_KV_NT 1
+#endif
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+ZK_DEV uint4 ld_kv(const bf16_t* p) {
+    if constexpr (ZK_KV_NT) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)));
+    else return *reinterpret_cast<const uint4*>(p);
+}
+
 ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int key_base, int ln, int lg) {
     (void)Smax;
     const int lane = lg * 16 + ln;
@@ -323,9 +334,9 @@ ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = *reinterpret_cast<const uint4*>(k0 + (h * 4 + ks) * 512);
+        for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = ld_kv(k0 + (h * 4 + ks) * 512);
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) f.v[dt] = *reinterpret_cast<const uint4*>(v0 + dt * 512);
+    for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld_kv(v0 + dt * 512);
 }
 
 struct AttnState {
