@@ -315,17 +315,19 @@ struct KVFrag {
     uint4 v[8];      // [d-tile]
 };
 
-// KV cache slices: read once per step (hundreds of MB, beyond L2 and MALL), so with ZK_KV_NT
-// they are loaded non-temporally
-#ifndef ZK_KV_NT
-#define ZK_KV_NT 1
-#endif
+// KV cache slices. NT: loaded non-temporally -- chosen by the host when one launch streams
+// >= KV_NT_BYTES of cache (B=64: 0.8 GB, read once per step, far beyond L2 and the MALL: nt 3.815
+// vs 3.954 ms per decode step); small caches (B=1: 4 MB per layer) stay MALL-resident across
+// steps and plain loads keep them there (1.32 vs 1.35 ms per step).
+constexpr double KV_NT_BYTES = 64e6;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+template <bool NT>
 ZK_DEV uint4 ld_kv(const bf16_t* p) {
-    if constexpr (ZK_KV_NT) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)));
+    if constexpr (NT) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)));
     else return *reinterpret_cast<const uint4*>(p);
 }
 
+template <bool NT>
 ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int key_base, int ln, int lg) {
     (void)Smax;
     const int lane = lg * 16 + ln;
@@ -334,9 +336,9 @@ ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = ld_kv(k0 + (h * 4 + ks) * 512);
+        for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = ld_kv<NT>(k0 + (h * 4 + ks) * 512);
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld_kv(v0 + dt * 512);
+    for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld_kv<NT>(v0 + dt * 512);
 }
 
 struct AttnState {
@@ -424,7 +426,7 @@ ZK_DEV void patch_kv(KVFrag& f, const uint32_t* s_kn, const uint16_t* s_vn, int 
 // reduces the split-K slabs of its own 4 query heads + 1 KV head (768 columns), applies RoPE,
 // keeps q in LDS and (the split that owns the newest key) stores the new K / V^T entries
 // before the key loop reads them. One launch per layer instead of two.
-template <bool FUSED, bool NEOX = false>
+template <bool FUSED, bool NEOX, bool KVNT>
 __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H,
                                                         int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
                                                         float* work, float scale, bf16_t* out, const int32_t* skip,
@@ -458,8 +460,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     const int pos = ctx - 1;
     const bool early = FUSED && kb1 > kb0;
     if (early) {      // the first TWO key blocks are in flight during the prologue
-        load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
-        load_kv(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
+        load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
+        load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
     }
     if constexpr (FUSED) {
         // pairs: [0, G*64) q of heads g*G.., then 64 k pairs, then 64 v pairs
@@ -530,12 +532,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if (kb1 > kb0) {
-        if (!early) load_kv(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
+        if (!early) load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         for (int it = kb0; it < kb1; it += 2) {
-            if (!(early && it == kb0)) load_kv(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
+            if (!(early && it == kb0)) load_kv<KVNT>(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
             if (FUSED) patch_kv(fa, s_kn, s_vn, it * AT_KB + 32 * w, pos, ln, lg);
             attn_step(st, fa, qf, it * AT_KB + 32 * w, ctx, scale, lg);
-            load_kv(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
+            load_kv<KVNT>(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
             if (it + 1 < kb1) {
                 if (FUSED) patch_kv(fb, s_kn, s_vn, (it + 1) * AT_KB + 32 * w, pos, ln, lg);
                 attn_step(st, fb, qf, (it + 1) * AT_KB + 32 * w, ctx, scale, lg);
@@ -786,7 +788,9 @@ extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt
                Smax / AT_KB);
     ZK_REQUIRE(nsplit == 1 || work != nullptr, "zk_attn_decode: nsplit > 1 needs the work buffer");
     const float scale = 1.0f / sqrtf((float)hd);
-    hipLaunchKernelGGL(k_attn_decode<false>, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream,
+    const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
+    auto kern = kvnt ? k_attn_decode<false, false, true> : k_attn_decode<false, false, false>;
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work,
                        scale, (bf16_t*)out, skip, nullptr, 0, nullptr);
     ZK_CHECK_LAUNCH("zk_attn_decode");
@@ -816,14 +820,12 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
 #else
     const bf16_t* dbgq = nullptr;
 #endif
-    if (rope_neox)
-        hipLaunchKernelGGL((k_attn_decode<true, true>), dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq,
-                           (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale,
-                           (bf16_t*)out, skip, part, gemm_nsplit, freqs);
-    else
-        hipLaunchKernelGGL((k_attn_decode<true, false>), dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream,
-                           dbgq, (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale,
-                           (bf16_t*)out, skip, part, gemm_nsplit, freqs);
+    const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
+    auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true> : k_attn_decode<true, true, false>)
+                          : (kvnt ? k_attn_decode<true, false, true> : k_attn_decode<true, false, false>);
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq, (bf16_t*)k_cache,
+                       (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out, skip, part,
+                       gemm_nsplit, freqs);
     ZK_CHECK_LAUNCH("zk_attn_decode_qkv");
     if (nsplit > 1) {
         hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, nsplit,

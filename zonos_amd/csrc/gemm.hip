@@ -242,7 +242,9 @@ constexpr int WS_LDSPF = 1;      // chunks published ahead of the one being mult
 constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 
-// decode split-K slab stores (read once by the consumer kernel): non-temporal with ZK_SLAB_NT
+// k_gemm_ws split-K slab stores (read once by the consumer kernel): non-temporal with ZK_SLAB_NT
+// (B=64: decode step 3.928 vs 3.959 ms; the B <= 8 GEMV keeps plain stores: its slabs are small
+// and nt cost 2.5 % per step at B=1)
 #ifndef ZK_SLAB_NT
 #define ZK_SLAB_NT 1
 #endif
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int m = lg * 4 + i;
-                if (m < M) st_slab(Cpart + (size_t)split * M * N + (size_t)m * N + n, sum[i]);
+                if (m < M) Cpart[(size_t)split * M * N + (size_t)m * N + n] = sum[i];   // (B <= 8: plain, measured)
             }
         }
     } else {
