@@ -125,6 +125,52 @@ def make_weights(cfg: BackboneCfg, seed: int = 0, head_scale: float = 1.0, devic
     return {k: v.to(torch.bfloat16).to(device) for k, v in out.items()}
 
 
+def make_copy_weights(cfg: BackboneCfg, seed: int = 0, copy_gain: float = 1.0, emb_gain: float = 1.0,
+                      eos_tokens: tuple = (), noise: float = 0.0, device="cpu") -> dict:
+    """Synthetic weights whose greedy decisions have LARGE margins, so that free-running greedy
+    codes are a meaningful bit-identical target across CPU and GPU (test fixtures only).
+
+    Backbone / norms / embeddings as make_weights (embeddings x ``emb_gain``). Each head k is a
+    "copy" map: with pi_k a seeded permutation of 0..1023, row j = copy_gain * E_k[pi_k(j)] /
+    sqrt(D) (+ ``noise`` * N(0, 1/D)), so the row whose pi_k(j) is codebook k's current input token
+    gets a logit ~ copy_gain * sqrt(D / 9) above the others (the hidden state's projection on that
+    embedding), while every other row sees only cross-embedding noise ~ copy_gain * N(0, 1). The
+    MASK input (1025, delay-pattern fill) is folded into row pi_k^-1(0). Head 0's EOS row is a
+    boosted copy of each of ``eos_tokens`` (2x, beats the -log(1024) EOS bias of model.py:333-334),
+    so a greedy chain emits EOS deterministically when cb0 reaches one of them (the first EOS is
+    resampled away and starts the 6-step hold-off, model.py:362-392; a later one is accepted); rows
+    1024 of heads 1..8 stay small (EOS is masked there, model.py:331). The decision margins are checked on the
+    reference's own run by tests/test_oracle_golden.py."""
+    W = {k: v.float() for k, v in make_weights(cfg, seed=seed).items()}
+    D = cfg.d_model
+    g = torch.Generator(device="cpu").manual_seed(seed * 7919 + 17)
+    for k in range(cfg.n_cb):
+        E = W[f"embeddings.{k}.weight"]
+        perm = torch.randperm(1024, generator=g)
+        H = copy_gain * E[perm] / math.sqrt(D)
+        H[int((perm == 0).nonzero())] += copy_gain * E[MASK] / math.sqrt(D)
+        r = torch.randn(1025, D, generator=g) / math.sqrt(D)
+        eos_row = 0.1 * r[EOS:EOS + 1]
+        if k == 0 and eos_tokens:
+            eos_row = 2.0 * copy_gain * E[list(eos_tokens)].sum(0, keepdim=True) / math.sqrt(D)
+        H = torch.cat([H, eos_row]) + noise * r
+        W[f"heads.{k}.weight"] = H
+        W[f"embeddings.{k}.weight"] = E * emb_gain
+    return {k: v.to(torch.bfloat16).to(device) for k, v in W.items()}
+
+
+def copy_chain(W: dict, cfg: BackboneCfg, k: int, token: int, n: int) -> list:
+    """The greedy chain of head k under make_copy_weights (test helper): next = argmax_j of the
+    copy rows for input ``token``, n steps."""
+    E = W[f"embeddings.{k}.weight"].float()
+    H = W[f"heads.{k}.weight"].float()[:1024]
+    out = []
+    for _ in range(n):
+        token = int(torch.argmax(H @ E[token]))
+        out.append(token)
+    return out
+
+
 def pad_heads(W: dict, cfg: BackboneCfg) -> dict:
     """pad_weight_ (zonos/utils.py:22-37): 1025 % 8 == 1 extra zero row -> 1026 rows."""
     W = dict(W)
@@ -426,6 +472,57 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
         trace["delayed"] = delayed.clone()
         trace["offset"] = offset
     return finalize(delayed, offset, P)
+
+
+def forced_steps(W, cfg: BackboneCfg, cond: torch.Tensor, delayed: torch.Tensor, P: int, windows, sp: dict,
+                 seed: int, row_base: int = 0, cfg_scale: float = 2.0, force_full_length: bool = True) -> dict:
+    """Teacher-forced decode steps on a given delayed-code history (test instrumentation).
+
+    For each window (s0, n): the cache is rebuilt by ONE prefill over cond + delayed[..., :P+1+s0]
+    (model.py:181-202 -- the prefill path of the reference on the forced history; its logits are
+    those of loop step s0), then steps s0+1 .. s0+n-1 run as single-token decodes
+    (model.py:118-142) fed from the same history. At every step the logits get the loop's bias
+    (model.py:332-334; step 0 = the prefill sample, no bias) and are sampled with the engine's noise
+    key (seed, step, draw 0, row_base + b) (sampling.py:232-328). EOS is never accepted
+    (force_full_length, the benchmark mode), so the EOS protocol does not enter. Returns {step:
+    (raw CFG logits fp32 [B,9,V], token [B,9], decision margin [B,9])}.
+    """
+    R, Lc, _ = cond.shape
+    B = R // 2
+    rp = float(sp["repetition_penalty"])
+    spk = {k: v for k, v in sp.items() if k != "repetition_penalty"}
+    out = {}
+    for s0, n in windows:
+        kv = KVCache(cfg, R, Lc + delayed.shape[2] + 9)
+        freqs = rope_table(16384, cfg.head_dim)
+        ids = delayed[..., :P + 1 + s0].repeat(2, 1, 1)
+        logits = compute_logits(W, cfg, torch.cat([cond, embed_codes(W, cfg, ids)], dim=1), kv, freqs, cfg_scale)
+        kv.seqlen_offset += Lc + P + 1 + s0
+        kv.lengths[:] += Lc + P + 1 + s0
+        for j in range(n):
+            s = s0 + j
+            off = P + 1 + s
+            if j > 0:
+                ids = delayed[..., off - 1:off].repeat(2, 1, 1)
+                logits = compute_logits(W, cfg, embed_codes(W, cfg, ids), kv, freqs, torch.tensor(cfg_scale))
+                kv.seqlen_offset += 1
+                kv.lengths[:] += 1
+            raw = logits.clone()
+            lg = logits.clone()
+            if s > 0:
+                lg[:, 1:, EOS] = -torch.inf
+                lg[:, 0, EOS] -= torch.log(torch.tensor(1024.0))
+            if force_full_length:
+                lg[:, 0, EOS] = -torch.inf
+            q = torch.from_numpy(exp_noise(seed, s, 0, B, cfg.n_cb, cfg.vocab, row_base))
+            dec = []
+            tok = sample(lg, q, generated_tokens=delayed[..., :off] if s > 0 else None,
+                         repetition_penalty=torch.full((B,), rp), decision=dec, **spk)
+            kind, arr = dec[-1]
+            top = arr.topk(2, dim=-1).values
+            m = (top[..., 0] - top[..., 1]) if kind == "logit" else torch.log(top[..., 0] / top[..., 1].clamp_min(1e-38))
+            out[s] = (raw, tok[..., 0], m.float())
+    return out
 
 
 def finalize(delayed: torch.Tensor, offset: int, P: int):

@@ -142,13 +142,18 @@ def build_ref_model(cfg, W):
 
 
 def run_generate(model, cond, prefix, B, max_new, sp, seed, logits_steps=0):
+    """Reference generate with the engine's noise; records the CFG logits of the first
+    ``logits_steps`` steps (an int) or of the given step indices (a tuple)."""
     NoiseCtl.seed = seed
     rec = []
     orig = model._compute_logits
+    n_call = [0]
 
     def rec_logits(*a, **k):
         out = orig(*a, **k)
-        if len(rec) < logits_steps:
+        i = n_call[0]
+        n_call[0] += 1
+        if (i < logits_steps) if isinstance(logits_steps, int) else (i in logits_steps):
             rec.append(out.clone())
         return out
 
@@ -215,6 +220,142 @@ def make_generate_fixtures():
         if rec:
             d["logits"] = torch.stack(rec).numpy().astype(np.float32)
         np.savez_compressed(os.path.join(HERE, f"gen_{name}.npz"), **d)
+
+
+def decision_margins(trace) -> np.ndarray:
+    """[steps, B, 9] min over the draws of a step of the oracle's top-1/top-2 decision margin
+    (logit units for greedy, log-ratio of probs/noise for sampling)."""
+    out = []
+    for dec in trace["decision"]:
+        ms = []
+        for kind, arr in dec:
+            top = arr.topk(2, dim=-1).values
+            ms.append((top[..., 0] - top[..., 1]) if kind == "logit"
+                      else torch.log(top[..., 0] / top[..., 1].clamp_min(1e-38)))
+        out.append(torch.stack(ms).min(dim=0).values.float())
+    return torch.stack(out).numpy()
+
+
+COPY_GAIN = 1.0
+COPY_FIX = {   # name: (sampling, weight seed, eos trigger steps of utterance 0's cb0 chain)
+    "copy_greedy": (GEN_CASES["greedy"]["sp"], 0, ()),
+    "copy_rep": (GEN_CASES["greedy_rep"]["sp"], 2, ()),      # seed 2: the penalty bites with margin
+    "copy_eos": (GEN_CASES["greedy"]["sp"], 0, (12, 24)),    # 1st EOS resampled (hold-off), 2nd accepted
+}
+
+
+def make_copy_fixtures():
+    """Free-running greedy fixtures on copy heads (zonos_ref.make_copy_weights) at D=1024, run by
+    the reference; the margins of every decision are stored for the tests to check."""
+    from tests.golden_util import COPY
+    cond = zonos_ref.synthetic_conditioning(GEN_B, GEN_LC, COPY.d_model, seed=1)
+    prefix = zonos_ref.synthetic_prefix_codes(GEN_B, GEN_P, seed=3)
+    for name, (sp, wseed, eos_steps) in COPY_FIX.items():
+        eos_tokens = ()
+        if eos_steps:
+            chain = zonos_ref.copy_chain(zonos_ref.make_copy_weights(COPY, seed=wseed, copy_gain=COPY_GAIN), COPY, 0,
+                                         int(prefix[0, 0, -1]), max(eos_steps) + 1)
+            eos_tokens = tuple(chain[i] for i in eos_steps)
+        W = zonos_ref.make_copy_weights(COPY, seed=wseed, copy_gain=COPY_GAIN, eos_tokens=eos_tokens)
+        model = build_ref_model(COPY, W)
+        seed = 1234
+        out, rec = run_generate(model, cond, prefix, GEN_B, GEN_NEW, sp, seed, 2)
+        trace = {}
+        out_o = zonos_ref.generate(zonos_ref.pad_heads(W, COPY), COPY, cond, prefix, GEN_NEW, 2.0, GEN_B, sp,
+                                   seed=seed, trace=trace)
+        same = len(out) == len(out_o) and all(torch.equal(a, b) for a, b in zip(out, out_o))
+        m = decision_margins(trace)
+        codes, lens = pack_codes(out)
+        print(f"[gen:{name}] lens={lens.tolist()} oracle_match={same} min margin {m.min():.3f}")
+        assert same, f"oracle diverges from reference on {name}"
+        d = dict(codes=codes, lens=lens, cond=cond.view(torch.int16).numpy(), prefix=prefix.numpy().astype(np.int16),
+                 seed=np.int64(seed), wsum=np.array(wsum(W)), wseed=np.int64(wseed), copy_gain=np.float32(COPY_GAIN),
+                 eos_tokens=np.array(eos_tokens, dtype=np.int64), max_new=np.int32(GEN_NEW),
+                 delayed=trace["delayed"].numpy().astype(np.int16), offset=np.int32(trace["offset"]),
+                 margins=m.astype(np.float32), logits=torch.stack(rec).numpy().astype(np.float32))
+        for k, v in sp.items():
+            d["sp_" + k] = np.float64(v)
+        np.savez_compressed(os.path.join(HERE, f"gen_{name}.npz"), **d)
+
+
+def ref_forced_steps(model, cond, delayed, P, windows, sp, seed, row_base):
+    """The reference's own prefill (model.py:181-202) over a forced history, then its single-token
+    decode (model.py:118-142), its logit bias (332-334, EOS never accepted: benchmark mode) and
+    sample_from_logits with the engine's noise key. Mirrors zonos_ref.forced_steps."""
+    import zonos.sampling as zs_
+    R, Lc, _ = cond.shape
+    B = R // 2
+    rp = float(sp["repetition_penalty"])
+    spk = {k: v for k, v in sp.items() if k != "repetition_penalty"}
+    out = {}
+    for s0, n in windows:
+        ip = model.setup_cache(batch_size=R, max_seqlen=Lc + delayed.shape[2] + 9)
+        logits = model._prefill(cond, delayed[..., :P + 1 + s0], ip, 2.0)
+        ip.seqlen_offset += Lc + P + 1 + s0
+        ip.lengths_per_sample[:] += Lc + P + 1 + s0
+        for j in range(n):
+            s = s0 + j
+            off = P + 1 + s
+            if j > 0:
+                logits = model._decode_one_token(delayed[..., off - 1:off], ip, torch.tensor(2.0), allow_cudagraphs=False)
+                ip.seqlen_offset += 1
+                ip.lengths_per_sample[:] += 1
+            raw = logits.clone()
+            lg = logits.clone()
+            if s > 0:
+                lg[:, 1:, 1024] = -torch.inf
+                lg[:, 0, 1024] -= torch.log(torch.tensor(1024.0))
+            lg[:, 0, 1024] = -torch.inf
+            NoiseCtl.seed, NoiseCtl.step, NoiseCtl.draw, NoiseCtl.row_base = seed, s, 0, row_base
+            tok = zs_.sample_from_logits(lg, generated_tokens=delayed[..., :off] if s > 0 else None,
+                                         repetition_penalty=torch.full((B,), rp), eos_token_id=1024, **spk)
+            out[s] = (raw.detach(), tok[..., 0].detach())
+    NoiseCtl.row_base = 0
+    return out
+
+
+def make_full_fixtures(which=("c1", "c2", "c3")):
+    """Full-width (D=2048, 26 layers) fixtures of SURVEY §8(d) c1/c2/c3, run by the reference
+    (about 5 min on 8 cores). c1: free-running greedy on copy heads. c2/c3: teacher-forced windows
+    on a seeded synthetic history, CLI sampling, random weights; only the utterances in `utts`."""
+    from tests.golden_util import CLI_SP, FULL, FULL_CASES, FULL_SEED, GREEDY_SP, forced_history, full_weights
+    for name in which:
+        c = FULL_CASES[name]
+        B, Lc, P, T = c["B"], c["Lc"], c["P"], c["T"]
+        cond = zonos_ref.synthetic_conditioning(B, Lc, FULL.d_model, seed=1)
+        prefix = zonos_ref.synthetic_prefix_codes(B, P, seed=3) if P else None
+        W = full_weights("copy" if name == "c1" else "random")
+        model = build_ref_model(FULL, {k: (v[:1025] if k.startswith("heads") else v) for k, v in W.items()})
+        d = dict(seed=np.int64(FULL_SEED))
+        if name == "c1":
+            out, rec = run_generate(model, cond, prefix, B, T, GREEDY_SP, FULL_SEED, tuple(c["logit_steps"]))
+            trace = {}
+            out_o = zonos_ref.generate(W, FULL, cond, prefix, T, 2.0, B, GREEDY_SP, seed=FULL_SEED, trace=trace)
+            same = all(torch.equal(a, b) for a, b in zip(out, out_o))
+            m = decision_margins(trace)
+            codes, lens = pack_codes(out)
+            print(f"[full c1] lens={lens.tolist()} oracle_match={same} min margin {m.min():.3f}")
+            assert same
+            d.update(codes=codes, lens=lens, margins=m.astype(np.float32), logits=torch.stack(rec).numpy(),
+                     delayed=trace["delayed"].numpy().astype(np.int16), offset=np.int32(trace["offset"]))
+        else:
+            hist = forced_history(B, P, T, prefix)
+            logits, toks, margins, steps = [], [], [], []
+            for u in c["utts"]:
+                cu = torch.cat([cond[u:u + 1], cond[B + u:B + u + 1]])
+                r = ref_forced_steps(model, cu, hist[u:u + 1], P, c["windows"], CLI_SP, FULL_SEED, u)
+                o = zonos_ref.forced_steps(W, FULL, cu, hist[u:u + 1], P, c["windows"], CLI_SP, FULL_SEED, u)
+                steps = sorted(r)
+                for s in steps:
+                    assert torch.equal(r[s][0], o[s][0]) and torch.equal(r[s][1], o[s][1]), (name, u, s)
+                logits.append(torch.stack([r[s][0][0] for s in c["logit_steps"]]))
+                toks.append(torch.stack([r[s][1][0] for s in steps]))
+                margins.append(torch.stack([o[s][2][0] for s in steps]))
+                print(f"[full {name}] utt {u}: {len(steps)} steps, oracle bit-exact, "
+                      f"min margin {float(torch.stack(margins[-1:]).min()):.3f}")
+            d.update(steps=np.array(steps, dtype=np.int32), logits=torch.stack(logits).numpy(),
+                     tokens=torch.stack(toks).numpy().astype(np.int16), margins=torch.stack(margins).numpy())
+        np.savez_compressed(os.path.join(HERE, f"gen_full_{name}.npz"), **d)
 
 
 SAMPLER_CASES = [
@@ -394,9 +535,17 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "cond":
         make_cond_fixtures()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "copy":
+        make_copy_fixtures()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "full":
+        make_full_fixtures(tuple(sys.argv[2:]) or ("c1", "c2", "c3"))
+        sys.exit(0)
     make_delay_fixtures()
     make_sampler_fixtures()
     make_generate_fixtures()
+    make_copy_fixtures()
+    make_full_fixtures()
     make_dac_fixtures()
     make_dac_encoder_fixture()
     make_cond_fixtures()

@@ -24,6 +24,66 @@ def load_enc_case():
 
 
 GEN_CASES = ["greedy", "greedy_rep", "sampled_cli", "sampled_knobs", "eos_greedy", "eos_sampled"]
+# free-running greedy fixtures on "copy" heads (zonos_ref.make_copy_weights): every decision that
+# reaches the output has a top-1/top-2 margin far above the GPU-vs-CPU logit error, so the codes
+# are a bit-identical target (D=1024 so the copy signal, ~sqrt(D/9), clears the cross-embedding
+# noise of 1025 rows)
+COPY = zonos_ref.BackboneCfg(d_model=1024, n_layer=2, n_heads=8, n_kv=2, d_ff=2048)
+COPY_CASES = ["copy_greedy", "copy_rep", "copy_eos"]
+FULL = zonos_ref.ZONOS_V01_TRANSFORMER
+CLI_SP = dict(top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
+              repetition_penalty_window=8, temperature=1.0)
+GREEDY_SP = dict(temperature=0.0, top_p=0, top_k=0, min_p=0, linear=0.0, conf=0.0, quad=0.0,
+                 repetition_penalty=1.0, repetition_penalty_window=2)
+# full-width (Zonos-v0.1-transformer geometry) workloads of SURVEY §8(d):
+#   c1: free-running greedy on copy heads (bit-identical codes, reference-generated);
+#   c2/c3: random weights (the bench's distribution), CLI sampling, teacher-forced on a seeded
+#          synthetic history; windows = (first step, steps) -- one prefill over the forced history,
+#          then single-token decodes; `utts` = utterances the reference computed.
+FULL_CASES = {
+    "c1": dict(B=1, Lc=24, P=0, T=129, emb_gain=4.0, logit_steps=(0, 1, 64, 128)),
+    "c2": dict(B=1, Lc=160, P=0, T=861, windows=((0, 32), (800, 8)), utts=(0,), logit_steps=(0, 1, 31, 800, 807)),
+    "c3": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 8), (1290, 8)), utts=(0, 37),
+               logit_steps=(0, 1, 1290, 1291)),
+}
+FULL_SEED = 1234
+
+
+def forced_history(B: int, P: int, T: int, prefix, seed: int = 7) -> torch.Tensor:
+    """Delayed codes [B, 9, T+9] of a seeded random history after the prefix (teacher forcing)."""
+    g = torch.Generator().manual_seed(seed)
+    codes = torch.randint(0, 1024, (B, 9, T), generator=g)
+    if P:
+        codes[..., :P] = prefix
+    return zonos_ref.apply_delay(codes)
+
+
+_W_CACHE = {}
+
+
+def full_weights(kind: str):
+    """Full-width weights (cached per process): 'random' = make_weights(FULL, 0), 'copy' = c1's."""
+    if kind not in _W_CACHE:
+        _W_CACHE.clear()
+        if kind == "random":
+            W = zonos_ref.make_weights(FULL, seed=0)
+        else:
+            W = zonos_ref.make_copy_weights(FULL, seed=0, emb_gain=FULL_CASES["c1"]["emb_gain"])
+        _W_CACHE[kind] = zonos_ref.pad_heads(W, FULL)
+    return _W_CACHE[kind]
+
+
+def load_full_case(name):
+    """gen_full_<name>.npz + its inputs (cond, prefix, forced history) rebuilt from their seeds."""
+    d = np.load(os.path.join(G, f"gen_full_{name}.npz"))
+    c = dict(FULL_CASES[name])
+    B, Lc, P = c["B"], c["Lc"], c["P"]
+    c["cond"] = zonos_ref.synthetic_conditioning(B, Lc, FULL.d_model, seed=1)
+    c["prefix"] = zonos_ref.synthetic_prefix_codes(B, P, seed=3) if P else None
+    c.update({k: d[k] for k in d.files})
+    if name != "c1":
+        c["history"] = forced_history(B, P, c["T"], c["prefix"])
+    return c
 
 
 def wsum(W: dict) -> str:
@@ -39,13 +99,20 @@ def load_gen_case(name):
     sp = {k[3:]: float(d[k]) for k in d.files if k.startswith("sp_")}
     sp["top_k"] = int(sp["top_k"])
     sp["repetition_penalty_window"] = int(sp["repetition_penalty_window"])
-    W_raw = zonos_ref.make_weights(TINY, seed=0, head_scale=float(d["head_scale"]), eos_bias=float(d["eos_bias"]))
+    if name.startswith("copy"):
+        cfg = COPY
+        W_raw = zonos_ref.make_copy_weights(COPY, seed=int(d["wseed"]), copy_gain=float(d["copy_gain"]),
+                                            eos_tokens=tuple(int(t) for t in d["eos_tokens"]))
+    else:
+        cfg = TINY
+        W_raw = zonos_ref.make_weights(TINY, seed=0, head_scale=float(d["head_scale"]), eos_bias=float(d["eos_bias"]))
     cond = torch.from_numpy(d["cond"]).view(torch.bfloat16)
-    return dict(W_raw=W_raw, W=zonos_ref.pad_heads(W_raw, TINY), wsum=str(d["wsum"]), cond=cond,
+    return dict(cfg=cfg, W_raw=W_raw, W=zonos_ref.pad_heads(W_raw, cfg), wsum=str(d["wsum"]), cond=cond,
                 prefix=torch.from_numpy(d["prefix"].astype(np.int64)), B=cond.shape[0] // 2,
                 max_new=int(d["max_new"]), seed=int(d["seed"]), sp=sp, codes=d["codes"], lens=d["lens"],
                 delayed=d["delayed"], offset=int(d["offset"]),
-                logits=d["logits"] if "logits" in d.files else None)
+                logits=d["logits"] if "logits" in d.files else None,
+                margins=d["margins"] if "margins" in d.files else None)
 
 
 # ---- PrefixConditioner fixtures (cond.npz; made by make_golden.make_cond_fixtures)

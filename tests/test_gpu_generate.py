@@ -6,16 +6,50 @@ import torch
 
 from oracle import zonos_ref
 
-from .golden_util import GEN_CASES, TINY, load_gen_case
+from .golden_util import COPY_CASES, GEN_CASES, TINY, load_gen_case
 
 pytestmark = pytest.mark.gpu
 
 
-def _engine(W):
+def _engine(W, cfg=TINY):
     from zonos_amd.engine import EngineConfig, HipDecoder
-    cfg = EngineConfig(d_model=TINY.d_model, n_layer=TINY.n_layer, n_heads=TINY.n_heads, n_kv=TINY.n_kv,
-                       d_ff=TINY.d_ff, eps=TINY.eps)
-    return HipDecoder(cfg, W, "cuda")
+    ec = EngineConfig(d_model=cfg.d_model, n_layer=cfg.n_layer, n_heads=cfg.n_heads, n_kv=cfg.n_kv,
+                      d_ff=cfg.d_ff, eps=cfg.eps)
+    return HipDecoder(ec, W, "cuda")
+
+
+def _output_positions(c):
+    """(step, b, k) decisions whose token reaches the golden history: everything except the
+    positions the EOS protocol overwrites with MASK/EOS (model.py:404-409)."""
+    P = c["prefix"].shape[2]
+    T = P + c["max_new"]
+    d = c["delayed"]
+    keep = np.ones((d.shape[2] - (P + 1), c["B"], 9), dtype=bool)
+    for s in range(keep.shape[0]):
+        t = P + 1 + s
+        gen = np.array([P <= t - k - 1 < T for k in range(9)])      # codes[k, t-k-1] is generated
+        keep[s] = (d[:, :, t] < 1024) & gen[None, :]
+    return keep
+
+
+@pytest.mark.parametrize("name", COPY_CASES)
+@pytest.mark.parametrize("graph", [True, False])
+def test_free_running_greedy_bit_identical(name, graph):
+    """Free-running greedy generate (no teacher forcing): the codes the reference generated,
+    bit for bit -- prefix + 40 steps of 3 utterances, EOS hold-off and acceptance (copy_eos),
+    repetition penalty biting (copy_rep). The fixture's decisions all have margins far above the
+    GPU-vs-CPU logit error (asserted here from the reference's own run)."""
+    c = load_gen_case(name)
+    keep = _output_positions(c)
+    m = c["margins"][:keep.shape[0]]
+    assert m[keep].min() > 2.0, m[keep].min()
+    eng = _engine(c["W"], c["cfg"])
+    out = eng.generate(c["cond"].cuda(), c["prefix"].cuda(), c["max_new"], 2.0, c["B"], c["sp"], seed=c["seed"],
+                       use_graph=graph, poll_every=5)
+    lens = [int(x.shape[1]) for x in out]
+    assert lens == c["lens"].tolist()
+    for i, x in enumerate(out):
+        assert np.array_equal(x.cpu().numpy(), c["codes"][i, :, :lens[i]]), i
 
 
 def _margins(decision):
@@ -36,21 +70,24 @@ def _margins(decision):
 TAU_LOGIT, TAU_LOGRATIO = 0.3, 0.3
 
 
-@pytest.mark.parametrize("name", GEN_CASES)
+@pytest.mark.parametrize("name", GEN_CASES + COPY_CASES)
 def test_generate_teacher_forced_matches_reference(name):
     """Every frame of the reference's generation (golden delayed codes) is reproduced by the
     HIP engine when it is fed the reference's own history (teacher forcing), at every
-    (step, utterance, codebook) whose decision margin exceeds the tolerance; EOS fill,
-    frame writes and trims are integer-exact."""
+    (step, utterance, codebook) whose decision margin exceeds the tolerance. The fraction of
+    decisions excused by the margin is asserted: <= 10 % on the copy-head greedy fixtures (the
+    north_star's greedy cases), and kept at its measured level on the random-head fixtures, whose
+    1026-way bf16 logits put 17-19 % (greedy) / 45 % (unified sampler, whose exponent multiplies
+    logit errors by ~3.4) of the decisions within reduction-order noise of a tie."""
     c = load_gen_case(name)
     gold = torch.from_numpy(c["delayed"]).long()
     # decision margins on the golden history, recomputed by the oracle on this host's CPU
     # (bf16 CPU kernels differ across CPU ISAs, so the margins, not the exact logits, travel)
     tr = {}
-    zonos_ref.generate(c["W"], TINY, c["cond"], c["prefix"], c["max_new"], 2.0, c["B"], c["sp"], seed=c["seed"],
+    zonos_ref.generate(c["W"], c["cfg"], c["cond"], c["prefix"], c["max_new"], 2.0, c["B"], c["sp"], seed=c["seed"],
                        trace=tr, force_delayed=gold)
     P = c["prefix"].shape[2]
-    eng = _engine(c["W"])
+    eng = _engine(c["W"], c["cfg"])
     stats = dict(checked=0, skipped=0, mismatch=[])
     diverged = set()
     # a logit error e moves log(p1/q1) - log(p2/q2) by up to e/T, times the unified
@@ -87,9 +124,14 @@ def test_generate_teacher_forced_matches_reference(name):
     thresholds = c["sp"].get("top_p", 0) > 0 or c["sp"].get("min_p", 0) > 0
     allowed = stats["checked"] // 200 if thresholds else 0
     assert len(stats["mismatch"]) <= allowed, stats["mismatch"][:10]
-    assert stats["checked"] > 0.5 * (stats["checked"] + stats["skipped"]), stats
-    print(name, {k: (v if k != "mismatch" else len(v)) for k, v in stats.items()})
+    frac = stats["skipped"] / (stats["checked"] + stats["skipped"])
+    print(name, {k: (v if k != "mismatch" else len(v)) for k, v in stats.items()}, f"skipped {100 * frac:.1f} %")
+    greedy = c["sp"]["temperature"] == 0
+    assert frac <= (0.10 if name.startswith("copy") else 0.25 if greedy else 0.50), frac
     if not diverged:
+        # the output trim (delay revert, first-EOS cut, >=1024 -> 0, model.py:437-457) on the
+        # forced history: integer-exact. (The codes themselves are forced here; free-running
+        # codes are compared in test_free_running_greedy_bit_identical.)
         lens = [int(x.shape[1]) for x in out]
         assert lens == c["lens"].tolist()
         for i, x in enumerate(out):

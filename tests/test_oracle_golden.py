@@ -10,7 +10,8 @@ import torch
 from oracle import dac_ref, zonos_ref
 from oracle.philox import exp_noise, philox4x32_10
 
-from .golden_util import COND_CASES, ENC_DAC, cond_case, GEN_CASES, TINY, TINY_DAC, load_enc_case, load_gen_case, wsum
+from .golden_util import (CLI_SP, COND_CASES, COPY_CASES, ENC_DAC, FULL, FULL_SEED, GEN_CASES, GREEDY_SP, TINY_DAC,
+                          cond_case, full_weights, load_enc_case, load_full_case, load_gen_case, wsum)
 
 G = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -55,12 +56,12 @@ def test_sampler_golden():
         assert np.array_equal(tok.squeeze(-1).numpy(), d[f"tok_{ci}"]), f"case {ci}"
 
 
-@pytest.mark.parametrize("name", list(GEN_CASES))
+@pytest.mark.parametrize("name", list(GEN_CASES) + COPY_CASES)
 def test_generate_golden(name):
     c = load_gen_case(name)
     assert wsum(c["W_raw"]) == c["wsum"], "synthetic weights are not reproducible on this host"
     trace = {}
-    out = zonos_ref.generate(c["W"], TINY, c["cond"], c["prefix"], c["max_new"], 2.0, c["B"], c["sp"],
+    out = zonos_ref.generate(c["W"], c["cfg"], c["cond"], c["prefix"], c["max_new"], 2.0, c["B"], c["sp"],
                              seed=c["seed"], trace=trace)
     assert [int(x.shape[1]) for x in out] == c["lens"].tolist()
     for i, x in enumerate(out):
@@ -106,3 +107,37 @@ def test_prefix_conditioner_golden(name):
     y = torch.cat([cond_ref.prefix_conditioner(c["W"], c["conds"], c["cond"], ids, c["proj"]),
                    cond_ref.prefix_conditioner(c["W"], c["conds"], c["uncond"], ids, c["proj"])])
     assert torch.equal(y, c["y"])
+
+
+def test_full_c1_golden():
+    """Full-width (1.62 B params) free-running greedy decode, B=1, Lc=24, 129 tokens: the oracle
+    reproduces the reference's codes and recorded logits bit for bit (~40 s on 8 cores)."""
+    c = load_full_case("c1")
+    trace = {}
+    out = zonos_ref.generate(full_weights("copy"), FULL, c["cond"], None, c["T"], 2.0, 1, GREEDY_SP,
+                             seed=FULL_SEED, trace=trace)
+    assert [int(x.shape[1]) for x in out] == c["lens"].tolist()
+    assert np.array_equal(out[0].numpy(), c["codes"][0, :, :c["lens"][0]])
+    got = np.stack([trace["logits"][s].numpy() for s in c["logit_steps"]])
+    assert np.array_equal(got, c["logits"])
+    assert c["margins"].min() > 6.0      # copy heads: every greedy decision far from a tie
+
+
+@pytest.mark.parametrize("name,window", [("c2", 0), ("c3", 0)])
+def test_full_forced_golden(name, window):
+    """Full-width teacher-forced steps (prefill over a forced history + single-token decodes,
+    CLI sampling with the engine's noise key) of utterance 0: the oracle reproduces the
+    reference's logits and tokens bit for bit (first window; the late-context windows were
+    cross-checked when the fixture was made)."""
+    c = load_full_case(name)
+    B, P = c["B"], c["P"]
+    s0, n = c["windows"][window]
+    cu = torch.cat([c["cond"][0:1], c["cond"][B:B + 1]])
+    o = zonos_ref.forced_steps(full_weights("random"), FULL, cu, c["history"][0:1], P, [(s0, n)], CLI_SP, FULL_SEED, 0)
+    steps = c["steps"].tolist()
+    for s, (raw, tok, m) in o.items():
+        j = steps.index(s)
+        assert np.array_equal(tok[0].numpy(), c["tokens"][0, j]), s
+        assert np.array_equal(m[0].numpy(), c["margins"][0, j]), s
+        if s in c["logit_steps"]:
+            assert np.array_equal(raw[0].numpy(), c["logits"][0, list(c["logit_steps"]).index(s)]), s

@@ -389,6 +389,11 @@ class HipDecoder:
         """fp32 CFG logits (before bias) of the last executed step [B][9][1026] (test hook)."""
         return self._ws["dbg"]
 
+    def last_tokens(self) -> torch.Tensor:
+        """Sampled tokens (first draw) of the last executed step, int32 [B][9] (test hook; the
+        frame may hold the delay pattern's MASK or a prefix code instead, model.py:305-306)."""
+        return self._ws["tok0"].view(-1, N_CB)
+
     def _capture(self, ws, B, st, sp, stream):
         if ws.get("graph"):
             call("zk_graph_destroy", ws["graph"])
