@@ -8,24 +8,28 @@ acceptance disabled so every row runs the full length, CLI sampling defaults; th
 DAC decoder (descript/dac_44khz geometry, seeded fp32 weights; fp16 conv operands with fp32
 accumulation = the reference's own GPU numerics, torch.autocast fp16 at autoencoder.py:46)
 turns all codes into waveforms. One "step" = generate() + DAC decode of the whole per-GPU
-batch.
+batch. Other configs: --batch 1 --lc 160 --prefix 0 --new-tokens 861 (c2), --model hybrid (c5).
 
-Multi-GPU: one process per GPU (torchrun), utterances sharded by rank (row_base keys the
-noise, so codes equal a single big batch), RCCL all_gather of the int32 codes at the end
-of each step; value = codes of all ranks / max-over-ranks wall time ("scaling": "weak").
+Multi-GPU: one process per GPU. `python bench.py --gpus N` starts torchrun itself (N ranks,
+127.0.0.1) before touching the GPU; under torchrun WORLD_SIZE must equal --gpus. Utterances
+are sharded by rank (row_base = rank * B keys the sampling noise), each rank runs its own
+engine with no data-path collective, and one RCCL all_gather of the int32 codes closes each
+step. Codes are shard-invariant as long as every shard has the same per-GPU batch (the GEMM
+reduction order depends on the M regime). value = codes of all ranks /
+max-over-ranks wall time ("scaling": "weak").
 
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0. `--stub` replaces the GPU workload by a CPU stand-in (gloo) so
+the launcher and the reporting path can be tested without a GPU (tests/test_bench_cpu.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -49,102 +53,174 @@ def parse():
     ap.add_argument("--no-dac", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=1)
+    ap.add_argument("--stub", action="store_true", help="CPU stand-in workload (launcher/reporting tests)")
     return ap.parse_args()
 
 
-def attn_roofline(eng, ctx, reps=50):
-    """Time the dominant kernel -- the decode attention with the fused in_proj epilogue
-    (zk_attn_decode_qkv), as the generate loop launches it -- with HIP events on its stream at
-    the workload's mean context. Algorithmic bytes per launch = K+V rows read (R*ctx*Hkv*hd*2*2)
-    + in_proj slabs read (nsplit*R*(H+2Hkv)*hd*4) + out write + new K/V write. traffic: the
-    PMC-measured HBM bytes per launch of the same kernel and shape, from the committed
-    rocprofv3 summary (profiles/*attn_pmc.json, tools/attn_pmc.py), or null."""
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int | None:
+    """--gpus N > 1 without a torchrun environment: run this script under torchrun (one rank per
+    GPU) as a CHILD process -- nothing here has touched the GPU yet -- and return its exit code."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world_env} but --gpus {args.gpus}")
+        return None
+    if args.gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------ rooflines
+def _time_launches(launches, reps=2):
+    """Average duration of the given launch closures (each called with the stream) with HIP
+    events on the engine's stream, after one warm pass. Returns seconds per launch."""
     import ctypes as C
 
     from zonos_amd import _lib
-    from zonos_amd._lib import call, ptr
-    ws = eng._ws
-    c = eng.cfg
-    R, Hk, hd, H = ws["R"], c.n_kv, c.head_dim, c.n_heads
-    gs = ws["splits"]["qkv"]
-    kc, vt = eng._kv(ws, c.n_layer // 2)
+    from zonos_amd._lib import call
     stream = _lib.stream_ptr()
     e0, e1 = _lib.P(), _lib.P()
     call("zk_event_create", C.byref(e0))
     call("zk_event_create", C.byref(e1))
-    args = (ptr(ws["part"]), gs, ptr(eng.freqs), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], ctx, None,
-            ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["y"]), 0, None, stream)
-    for _ in range(5):
-        call("zk_attn_decode_qkv", *args)
+    for f in launches:
+        f(stream)
     call("zk_event_record", e0.value, stream)
     for _ in range(reps):
-        call("zk_attn_decode_qkv", *args)
+        for f in launches:
+            f(stream)
     call("zk_event_record", e1.value, stream)
     ms = C.c_float()
     call("zk_event_elapsed_ms", e0.value, e1.value, C.byref(ms))
     call("zk_event_destroy", e0.value)
     call("zk_event_destroy", e1.value)
-    per_launch_s = ms.value / 1e3 / reps
-    Nq = (H + 2 * Hk) * hd
-    bytes_per_launch = R * ctx * Hk * hd * 2 * 2 + gs * R * Nq * 4 + R * H * hd * 2 + R * Hk * hd * 2 * 2
-    ach = bytes_per_launch / per_launch_s / 1e9
-    traffic = None
+    return ms.value / 1e3 / (reps * len(launches))
+
+
+def _pmc_traffic(kernel_prefix: str, **shape):
+    """HBM bytes per launch from the committed rocprofv3 PMC summaries (profiles/*pmc*.json,
+    written by tools/attn_pmc.py / tools/gemm_pmc.py), matching kernel name prefix and shape."""
     import glob
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*attn*pmc*.json"))):
-        d = json.load(open(f))
-        if d.get("R") == R and d.get("ctx") == ctx and d.get("kernel") == "k_attn_decode<true>":
-            traffic = d["hbm_bytes_per_launch"]
+    found = None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+        for e in (d if isinstance(d, list) else [d]):
+            if str(e.get("kernel", "")).startswith(kernel_prefix) and all(e.get(k) == v for k, v in shape.items()):
+                found = e["hbm_bytes_per_launch"]
+    return found
+
+
+def _roof(bytes_per_launch, per_launch_s, **extra):
+    ach = bytes_per_launch / per_launch_s / 1e9
     return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                traffic=traffic, kernel="k_attn_decode<true> (zk_attn_decode_qkv)" +
-                ("+k_attn_combine" if ws["attn_splits"] > 1 else ""),
-                ctx=ctx, attn_splits=ws["attn_splits"],
-                bytes_per_launch=bytes_per_launch, us_per_launch=round(per_launch_s * 1e6, 2))
+                bytes_per_launch=int(bytes_per_launch), us_per_launch=round(per_launch_s * 1e6, 2), **extra)
 
 
-def mamba_roofline(eng, reps=50):
-    """Hybrid: time zk_mamba_step (the SSM state update, HBM-bound) of one Mamba layer with HIP
-    events; algorithmic bytes = SSM state read + write (R*d_inner*d_state*2 B each) + conv
-    state read + write + in_proj slabs read + yz write."""
-    import ctypes as C
+def attn_roofline(eng, ctx):
+    """Decode attention with the fused in_proj epilogue (zk_attn_decode_qkv), launched as the
+    generate loop launches it, over the 26 layers' own KV caches in turn at the workload's mean
+    context. Algorithmic bytes per launch = K+V rows read (R*ctx*Hkv*hd*2*2) + in_proj slabs read
+    (nsplit*R*(H+2Hkv)*hd*4) + output write + new K/V write."""
+    from zonos_amd._lib import call, ptr
+    ws, c = eng._ws, eng.cfg
+    R, Hk, hd, H = ws["R"], c.n_kv, c.head_dim, c.n_heads
+    gs = ws["splits"]["qkv"]
 
-    from zonos_amd import _lib
+    def launch(layer):
+        kc, vt = eng._kv(ws, layer)
+        return lambda st: call("zk_attn_decode_qkv", ptr(ws["part"]), gs, ptr(eng.freqs), ptr(kc), ptr(vt), R, H, Hk,
+                               hd, ws["smax"], ctx, None, ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["y"]),
+                               eng.rope_neox, None, st)
+    layers = getattr(eng, "attn_ids", range(c.n_layer))
+    per = _time_launches([launch(i) for i in layers], reps=4)
+    Nq = (H + 2 * Hk) * hd
+    b = R * ctx * Hk * hd * 2 * 2 + gs * R * Nq * 4 + R * H * hd * 2 + R * Hk * hd * 2 * 2
+    return _roof(b, per, traffic=_pmc_traffic("k_attn_decode<true", R=R, ctx=ctx),
+                 kernel="k_attn_decode<true> (zk_attn_decode_qkv)" + ("+k_attn_combine" if ws["attn_splits"] > 1 else ""),
+                 ctx=ctx, attn_splits=ws["attn_splits"], layers="rotating over all attention layers' caches")
+
+
+def gemv_roofline(eng):
+    """B <= 8 (c2): the weight-streaming fc1 GEMV + SwiGLU epilogue (zk_gemm_bf16 -> k_gemv_rk, the
+    largest launch of the step), over the 26 layers' fc1 weights in turn (67 MB each: nothing stays
+    in L2/MALL between launches, as in the real step). Bytes = weights + activation + output."""
+    from zonos_amd._lib import call, ptr
+    ws, c = eng._ws, eng.cfg
+    R, D, Fd = ws["R"], c.d_model, c.d_ff
+
+    def launch(L):
+        return lambda st: call("zk_gemm_bf16", ptr(ws["xn"]), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, 1, None,
+                               ptr(ws["h"]), None, st)
+    per = _time_launches([launch(L) for L in eng.layers if "fc1" in L], reps=4)
+    b = 2 * Fd * D * 2 + R * D * 2 + R * Fd * 2
+    return _roof(b, per, traffic=_pmc_traffic("k_gemv_rk", R=R, N=2 * Fd, K=D),
+                 kernel="k_gemv_rk (zk_gemm_bf16 fc1 + SwiGLU)", M=R, N=2 * Fd, K=D,
+                 layers="rotating over all layers' fc1 weights")
+
+
+def mamba_roofline(eng):
+    """Hybrid (c5): zk_mamba_step (the SSM state update, HBM-bound) over every Mamba layer's state
+    in turn; algorithmic bytes = SSM state read + write (R*d_inner*d_state*2 B each) + conv state
+    read + write + in_proj slabs read + yz write."""
     from zonos_amd._lib import call, ptr
     ws, c = eng._ws, eng.cfg
     R = ws["R"]
-    j = len(eng.mamba_ids) // 2
-    L = eng.layers[eng.mamba_ids[j]]
-    stream = _lib.stream_ptr()
-    e0, e1 = _lib.P(), _lib.P()
-    call("zk_event_create", C.byref(e0))
-    call("zk_event_create", C.byref(e1))
     gs = ws["splits"]["inp"]
-    args = (ptr(ws["part"]), gs, R, c.d_inner, c.nheads_ssm, c.headdim, c.d_state, ptr(L["conv_w"]),
-            ptr(L["conv_b"]), ptr(ws["conv"][j][0]), ptr(ws["conv"][j][1]), ptr(ws["scal"][1:2]), ptr(ws["ssm"][j]),
-            ptr(L["A"]), ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), None, stream)
-    for _ in range(5):
-        call("zk_mamba_step", *args)
-    call("zk_event_record", e0.value, stream)
-    for _ in range(reps):
-        call("zk_mamba_step", *args)
-    call("zk_event_record", e1.value, stream)
-    ms = C.c_float()
-    call("zk_event_elapsed_ms", e0.value, e1.value, C.byref(ms))
-    call("zk_event_destroy", e0.value)
-    call("zk_event_destroy", e1.value)
-    per = ms.value / 1e3 / reps
-    b = (R * c.d_inner * c.d_state * 2 * 2 + R * c.conv_dim * 8 * 2 + gs * R * c.d_in_proj * 4 + R * c.d_inner * 4)
-    ach = b / per / 1e9
-    return dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
-                traffic=None, kernel="k_mamba_step", bytes_per_launch=b, us_per_launch=round(per * 1e6, 2))
+
+    def launch(j):
+        L = eng.layers[eng.mamba_ids[j]]
+        return lambda st: call("zk_mamba_step", ptr(ws["part"]), gs, R, c.d_inner, c.nheads_ssm, c.headdim,
+                               c.d_state, ptr(L["conv_w"]), ptr(L["conv_b"]), ptr(ws["conv"][j][0]),
+                               ptr(ws["conv"][j][1]), ptr(ws["scal"][1:2]), ptr(ws["ssm"][j]), ptr(L["A"]),
+                               ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), None, st)
+    per = _time_launches([launch(j) for j in range(len(eng.mamba_ids))], reps=4)
+    b = R * c.d_inner * c.d_state * 2 * 2 + R * c.conv_dim * 8 * 2 + gs * R * c.d_in_proj * 4 + R * c.d_inner * 4
+    return _roof(b, per, traffic=_pmc_traffic("k_mamba_step", R=R), kernel="k_mamba_step",
+                 layers="rotating over all Mamba layers' states")
 
 
+def step_bytes(eng, R: int, ctx: float) -> float:
+    """Algorithmic HBM bytes of one decode step at context ctx: every weight once
+    (bf16 GEMM weights, LayerNorms, heads) + the KV cache read (R*ctx rows) and written (R rows);
+    hybrid: + every Mamba layer's SSM state read and written and conv state."""
+    c = eng.cfg
+    D, H, Hk, hd = c.d_model, c.n_heads, c.n_kv, c.head_dim
+    attn_layer = (H + 2 * Hk) * hd * D + D * H * hd + 3 * c.d_ff * D + 4 * D
+    kv_row = 2 * Hk * hd * 2
+    n_attn = len(getattr(eng, "attn_ids", range(c.n_layer)))
+    b = 2 * (n_attn * attn_layer + 2 * D + 9 * 1026 * D) + n_attn * kv_row * R * (ctx + 1)
+    if hasattr(eng, "mamba_ids"):
+        nm = len(eng.mamba_ids)
+        b += 2 * nm * (c.d_in_proj * D + D * c.d_inner + c.d_inner + 2 * D + c.conv_dim * 5 + 3 * c.nheads_ssm)
+        b += nm * R * (2 * c.d_inner * c.d_state * 2 + 2 * c.conv_dim * 4 * 2)
+    return b
+
+
+# ------------------------------------------------------------------------------ CPU baseline
 def cpu_baseline(args):
     """Oracle (CPU restatement, validated against the reference) timed on this host: decode
     steps at B=64 at 3 context lengths (KV cache pre-filled) + a 43-frame DAC decode; scaled
-    to codes/s of the same workload (prefill excluded, <1% of the GPU time)."""
+    to codes/s of the same workload (prefill excluded, <1% of the GPU time). Threads = the
+    box's CPU share (16 per GPU)."""
+    import torch
+
     from oracle import dac_ref, zonos_ref
-    cores = os.cpu_count() or 1
-    threads = min(cores, 64)
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", 16)), 16)
     torch.set_num_threads(threads)
     cfg = zonos_ref.ZONOS_V01_TRANSFORMER
     W = zonos_ref.pad_heads(zonos_ref.make_weights(cfg, seed=0), cfg)
@@ -180,120 +256,192 @@ def cpu_baseline(args):
     total_s = N * step_s + B * args.new_tokens * dac_s_per_frame
     codes_total = B * args.new_tokens * 9
     return dict(value=round(codes_total / total_s, 2), unit="codes/s", cores=threads, kind="port",
-                sample=f"oracle decode step B={B} at ctx {ctx0 + int(0.1 * N)}/{ctx0 + int(0.5 * N)}/"
-                       f"{ctx0 + int(0.9 * N)} x{args.cpu_sample_steps} (mean {step_s:.3f} s/step) + DAC 43 frames "
-                       f"({dac_s_per_frame * 1e3:.1f} ms/frame); scaled to {N} steps + {B * args.new_tokens} frames; "
-                       f"{time.time() - t_begin - t_setup:.1f} s of timed CPU work (+{t_setup:.1f} s setup)",
+                sample=f"oracle decode step B={B} at ctx {ctxs[0]}/{ctxs[1]}/{ctxs[2]} x{args.cpu_sample_steps} "
+                       f"(mean {step_s:.3f} s/step) + DAC 43 frames ({dac_s_per_frame * 1e3:.1f} ms/frame); scaled to "
+                       f"{N} steps + {B * args.new_tokens} frames; {time.time() - t_begin - t_setup:.1f} s of timed "
+                       f"CPU work (+{t_setup:.1f} s setup)",
                 step_s=round(step_s, 4), dac_ms_per_frame=round(dac_s_per_frame * 1e3, 2))
+
+
+# ------------------------------------------------------------------------------ workloads
+class StubWorkload:
+    """CPU stand-in with the real workload's interface: 'generates' B utterances of new_tokens
+    frames per step (a short sleep) and gathers them over gloo like the codes gather."""
+
+    def __init__(self, args, rank, world, dist):
+        import torch
+        self.args, self.rank, self.dist, self.torch = args, rank, dist, torch
+        self.stats = {"gen_s": 0.0, "dac_s": 0.0}
+        self.model_name = "stub"
+
+    def step(self, i, timed):
+        torch = self.torch
+        B, T = self.args.batch, self.args.new_tokens
+        time.sleep(0.01 * (1 + self.rank))
+        codes = [torch.full((9, T), self.rank * B + b, dtype=torch.int64) for b in range(B)]
+        if self.dist is not None:
+            from zonos_amd.distributed import gather_codes
+            allc = gather_codes(codes)
+            assert len(allc) == B * self.dist.get_world_size()
+        return B * T
+
+    def sync(self):
+        pass
+
+    def report(self, elapsed, args):
+        return {}
+
+
+class GpuWorkload:
+    def __init__(self, args, rank, world, dist, dev):
+        import torch
+
+        from zonos_amd import synthetic
+        from zonos_amd.autoencoder import DacSpec, HipDacDecoder
+        from zonos_amd.engine import EngineConfig, HipDecoder
+        self.torch, self.args, self.rank, self.world, self.dist, self.dev = torch, args, rank, world, dist, dev
+        if args.model == "hybrid":
+            from zonos_amd.hybrid import HybridDecoder, HybridEngineConfig
+            mc = dict(synthetic.ZONOS_V01_HYBRID)
+            if args.layers:
+                mc["n_layer"] = args.layers
+                mc["attn_layer_idx"] = tuple(i for i in mc["attn_layer_idx"] if i < args.layers)
+            W = synthetic.hybrid_weights(dev, seed=0, **mc)
+            self.eng = HybridDecoder(HybridEngineConfig(**mc), W, dev)
+        else:
+            mc = dict(synthetic.ZONOS_V01, n_layer=args.layers or 26)
+            W = synthetic.backbone_weights(dev, seed=0, **mc)
+            self.eng = HipDecoder(EngineConfig(**mc), W, dev)
+        del W
+        self.mc = mc
+        self.dac = None if args.no_dac else HipDacDecoder(DacSpec(), synthetic.dac_weights(dev), dev)
+        B = args.batch
+        self.cond = synthetic.conditioning(B, args.lc, mc["d_model"], seed=1 + rank, device=dev)
+        self.prefix = synthetic.prefix_codes(B, args.prefix, seed=3 + rank, device=dev) if args.prefix else None
+        self.sp = dict(top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
+                       repetition_penalty_window=8, temperature=1.0)
+        self.stats = {"gen_s": 0.0, "dac_s": 0.0}
+        self.model_name = ("Zonos-v0.1-transformer" if args.model == "transformer"
+                           else "Zonos-v0.1-hybrid (assumed geometry)")
+
+    def step(self, i, timed):
+        torch, args = self.torch, self.args
+        t0 = time.time()
+        codes = self.eng.generate(self.cond, self.prefix, args.new_tokens, 2.0, args.batch, self.sp, seed=1000 + i,
+                                  row_base=self.rank * args.batch, force_full_length=True, poll_every=64)
+        torch.cuda.synchronize(self.dev)
+        t1 = time.time()
+        if self.dac is not None:
+            self.dac.decode_list(codes)
+        torch.cuda.synchronize(self.dev)
+        t2 = time.time()
+        if self.dist is not None:
+            from zonos_amd.distributed import gather_codes
+            gather_codes(codes, device=self.dev)
+        if timed:
+            self.stats["gen_s"] += t1 - t0
+            self.stats["dac_s"] += t2 - t1
+        return sum(int(c.shape[1]) for c in codes)
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def report(self, elapsed, args):
+        eng = self.eng
+        R = 2 * args.batch
+        n_dec = args.new_tokens + 8                       # decode steps per generate (max_steps)
+        ctx_mean = args.lc + args.prefix + 1 + n_dec // 2
+        if args.model == "hybrid":
+            roof = mamba_roofline(eng)
+        elif R <= 16:
+            roof = gemv_roofline(eng)
+        else:
+            roof = attn_roofline(eng, ctx_mean)
+        gen_step_s = self.stats["gen_s"] / args.steps
+        dec_ms = gen_step_s / n_dec * 1e3
+        sb = step_bytes(eng, R, ctx_mean)
+        step_roof = dict(bytes_per_step=int(sb), ctx_mean=ctx_mean, ms_per_decode_step=round(dec_ms, 4),
+                         achieved=round(sb / (dec_ms / 1e3) / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                         frac=round(sb / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                         note="algorithmic bytes per decode step at the mean context / (generate wall time / decode "
+                              "steps, prefill included)")
+        return dict(roofline=roof, step_roofline=step_roof,
+                    breakdown={"generate_s_per_step": round(gen_step_s, 3),
+                               "dac_s_per_step": round(self.stats["dac_s"] / args.steps, 3),
+                               "dac_precision": self.dac.precision if self.dac is not None else None,
+                               "decode_ms_per_token_step": round(dec_ms, 3)})
 
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    import torch
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-
-    from zonos_amd import synthetic
-    from zonos_amd.autoencoder import DacSpec, HipDacDecoder
-    from zonos_amd.engine import EngineConfig, HipDecoder
-
-    if args.model == "hybrid":
-        from zonos_amd.hybrid import HybridDecoder, HybridEngineConfig
-        mc = dict(synthetic.ZONOS_V01_HYBRID)
-        if args.layers:
-            mc["n_layer"] = args.layers
-            mc["attn_layer_idx"] = tuple(i for i in mc["attn_layer_idx"] if i < args.layers)
-        W = synthetic.hybrid_weights(dev, seed=0, **mc)
-        eng = HybridDecoder(HybridEngineConfig(**mc), W, dev)
+    if args.stub:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        wl = StubWorkload(args, rank, world, dist)
     else:
-        mc = dict(synthetic.ZONOS_V01, n_layer=args.layers or 26)
-        W = synthetic.backbone_weights(dev, seed=0, **mc)
-        eng = HipDecoder(EngineConfig(**mc), W, dev)
-    del W
-    dac = None if args.no_dac else HipDacDecoder(DacSpec(), synthetic.dac_weights(dev), dev)
-    B = args.batch
-    cond = synthetic.conditioning(B, args.lc, mc["d_model"], seed=1 + rank, device=dev)
-    prefix = synthetic.prefix_codes(B, args.prefix, seed=3 + rank, device=dev) if args.prefix else None
-    sp = dict(top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
-              repetition_penalty_window=8, temperature=1.0)
-    stats = {"gen_s": 0.0, "dac_s": 0.0}
-
-    def step(i, timed):
-        t0 = time.time()
-        codes = eng.generate(cond, prefix, args.new_tokens, 2.0, B, sp, seed=1000 + i, row_base=rank * B,
-                             force_full_length=True, poll_every=64)
-        torch.cuda.synchronize(dev)
-        t1 = time.time()
-        if dac is not None:
-            dac.decode_list(codes)
-        torch.cuda.synchronize(dev)
-        t2 = time.time()
-        if dist is not None:
-            from zonos_amd.distributed import gather_codes
-            gather_codes(codes, device=dev)
-        if timed:
-            stats["gen_s"] += t1 - t0
-            stats["dac_s"] += t2 - t1
-        return sum(int(c.shape[1]) for c in codes)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl", device_id=dev)
+        wl = GpuWorkload(args, rank, world, dist, dev)
 
     for i in range(args.warmup):
-        step(i, False)
+        wl.step(i, False)
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    wl.sync()
     t0 = time.time()
     frames = 0
     for i in range(args.steps):
-        frames += step(args.warmup + i, True)
-    torch.cuda.synchronize(dev)
+        frames += wl.step(args.warmup + i, True)
+    wl.sync()
     if dist is not None:
         dist.barrier()
     elapsed = time.time() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], device=dev)
+        dev_ = "cpu" if args.stub else torch.device("cuda", local)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev_)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        fr = torch.tensor([frames], device=dev, dtype=torch.float64)
+        fr = torch.tensor([frames], dtype=torch.float64, device=dev_)
         dist.all_reduce(fr)
         frames = int(fr.item())
 
     if rank == 0:
         codes_s = frames * 9 / elapsed
         audio_s = frames / FRAME_RATE
-        ctx_mean = args.lc + args.prefix + 1 + (args.new_tokens + 8) // 2
-        roof = attn_roofline(eng, ctx_mean) if args.model == "transformer" else mamba_roofline(eng)
-        model = "Zonos-v0.1-transformer" if args.model == "transformer" else "Zonos-v0.1-hybrid (assumed geometry)"
+        B = args.batch
         cfg_name = {(64, 400, 10, 2580): "c3", (1, 160, 0, 861): "c2"}.get(
             (args.batch, args.lc, args.prefix, args.new_tokens), "custom")
         if args.model == "hybrid" and cfg_name == "c3":
             cfg_name = "c5"
+        if cfg_name == "c3" and world > 1:
+            cfg_name = "c4" if world == 8 else f"c3x{world}"
         workload = (f"{cfg_name}: B={B}/GPU, Lc={args.lc}, prefix {args.prefix}, {args.new_tokens} new tokens "
                     f"({args.new_tokens / FRAME_RATE:.0f} s), EOS disabled, CLI sampling (linear .65 conf .4 rep "
                     f"2.5/8), DAC decode of all codes")
         out = {
-            "metric": f"DAC codes/sec (end-to-end generate + DAC decode), {model} batch={B}/GPU",
+            "metric": f"DAC codes/sec (end-to-end generate + DAC decode), {wl.model_name} batch={B}/GPU",
             "value": round(codes_s, 1), "unit": "codes/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded random weights + LayerNorm'd random conditioning; no checkpoint offline)",
-            "config": {"workload": workload, "model": model, "global_batch": B * world,
+            "config": {"workload": workload, "model": wl.model_name, "global_batch": B * world,
                        "seq_len": args.lc + args.prefix + args.new_tokens + 9, "parallelism": f"dp{world}"},
             "rtf": round(audio_s / elapsed, 2),
-            "breakdown": {"generate_s_per_step": round(stats["gen_s"] / args.steps, 3),
-                          "dac_s_per_step": round(stats["dac_s"] / args.steps, 3),
-                          "dac_precision": dac.precision if dac is not None else None,
-                          "generate_codes_s": round(frames / world * 9 / max(stats["gen_s"], 1e-9) * world, 1),
-                          "decode_ms_per_token_step": round(stats["gen_s"] / args.steps / (args.new_tokens + 8) * 1e3,
-                                                            3)},
-            "roofline": roof,
         }
-        if not args.no_cpu_baseline and world == 1 and args.model == "transformer":
+        out.update(wl.report(elapsed, args))
+        if not args.stub and not args.no_cpu_baseline and world == 1 and args.model == "transformer":
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -656,6 +656,11 @@ def _load_safetensors_dir(path: str):
 
 
 def _load_hf_cache(repo_id: str):
+    """The DAC weights the reference fetches by name (autoencoder.py:15): $ZONOS_DAC_PATH (a local
+    HF-format directory or .safetensors file) if set, else the local Hugging Face cache."""
+    local = os.environ.get("ZONOS_DAC_PATH")
+    if local:
+        return _load_safetensors_dir(local)
     from huggingface_hub import snapshot_download
     try:
         d = snapshot_download(repo_id, local_files_only=True)

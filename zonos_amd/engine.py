@@ -103,10 +103,12 @@ def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> in
     return max(1, min(want, cap, smax // 128))
 
 
-class HipDecoder:
-    """Owns device weights in engine layout and runs generate() on the GPU."""
+class HipBackbone:
+    """The 26 transformer blocks + final LayerNorm on the device (zonos/backbone/_torch.py:52-152):
+    bf16 weights in the engine's layouts and the layer launch sequence. Shared by the generate()
+    engine (HipDecoder) and the backbone plugin (zonos_amd.backbone.HipZonosBackbone)."""
 
-    def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
+    def __init__(self, cfg: EngineConfig, weights: dict, device="cuda", prefix: str = "backbone."):
         _lib.load()
         self.cfg = cfg
         self.fuse_qkv = True      # in_proj epilogue inside the decode attention launch (False: separate kernel)
@@ -117,22 +119,13 @@ class HipDecoder:
         dev = self.device
 
         def w(name):
-            t = weights[name]
+            t = weights[prefix + name]
             return t.to(device=dev, dtype=bf).contiguous()
 
-        self.emb = torch.stack([w(f"embeddings.{k}.weight") for k in range(N_CB)]).contiguous()
-        assert self.emb.shape == (N_CB, VOCAB, c.d_model), self.emb.shape
-        heads = []
-        for k in range(N_CB):
-            h = w(f"heads.{k}.weight")
-            if h.shape[0] < VOCAB:      # pad_weight_ (utils.py:22-37): 1025 -> 1026 rows
-                h = torch.cat([h, h.new_zeros(VOCAB - h.shape[0], h.shape[1])])
-            heads.append(h)
         stream = _lib.stream_ptr(dev)
-        self.heads = pack_weights(torch.cat(heads).contiguous(), stream)    # [9*1026 -> 9280][D] packed
         self.layers = []
         for i in range(c.n_layer):
-            p = f"backbone.layers.{i}."
+            p = f"layers.{i}."
             fc1 = w(p + "mlp.fc1.weight")
             fc1p = torch.empty_like(fc1)
             call("zk_permute_fc1", ptr(fc1), c.d_ff, c.d_model, ptr(fc1p), stream)
@@ -143,9 +136,76 @@ class HipDecoder:
                 wo=pack_weights(w(p + "mixer.out_proj.weight"), stream),
                 ln2_w=w(p + "norm2.weight"), ln2_b=w(p + "norm2.bias"),
                 fc1=pack_weights(fc1p, stream), fc2=pack_weights(w(p + "mlp.fc2.weight"), stream)))
-        self.lnf_w = w("backbone.norm_f.weight")
-        self.lnf_b = w("backbone.norm_f.bias")
+        self.lnf_w = w("norm_f.weight")
+        self.lnf_b = w("norm_f.bias")
         self.freqs = rope_table(16384, c.head_dim).to(dev)
+
+    def _kv(self, ws, layer):
+        if "kv_layers" in ws:            # caches handed out per layer (backbone plugin)
+            kv = ws["kv_layers"][layer]
+            return kv[0], kv[1]
+        return ws["kv"][layer, 0], ws["kv"][layer, 1]
+
+    # ------------------------------------------------------------------ transformer passes
+    def _layers(self, ws, M: int, R: int, S: int, prefill: bool, stream, skip):
+        """Run the 26 blocks on xn/x (rows = R*S). Leaves norm_f(x) in ws['xn']."""
+        c = self.cfg
+        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+        Nqkv = (H + 2 * Hk) * hd
+        sp = ws["splits"] if not prefill else dict(qkv=1, o=1, fc2=1)
+        x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
+        scal = ws["scal"]
+        pos_dev = None if prefill else ptr(scal[1:2])
+        for i, L in enumerate(self.layers):
+            kc, vt = self._kv(ws, i)
+            call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
+            if prefill:
+                call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
+                     ptr(kc), ptr(vt), ws["smax"], None, self.rope_neox, skip, stream)
+                call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
+            elif self.fuse_qkv:
+                # in_proj epilogue fused into the attention launch (position = ctx - 1 = scal[1])
+                call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), self.rope_neox,
+                     skip, stream)
+            else:
+                call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
+                     ptr(kc), ptr(vt), ws["smax"], None, self.rope_neox, skip, stream)
+                call("zk_attn_decode", ptr(q), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1, ptr(scal[1:2]),
+                     ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), skip, stream)
+            call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip, stream)
+            call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D, ptr(x),
+                 ptr(xn), 0, skip, stream)
+            call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fd, D, 1, 1, None, ptr(h), skip, stream)
+            call("zk_gemm_bf16", ptr(h), Fd, ptr(L["fc2"]), M, D, Fd, sp["fc2"], 0, ptr(part), None, skip, stream)
+            if i + 1 < len(self.layers):
+                nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
+            else:
+                nw, nb = self.lnf_w, self.lnf_b
+            call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 0, skip,
+                 stream)
+
+
+class HipDecoder(HipBackbone):
+    """Owns device weights in engine layout and runs generate() on the GPU."""
+
+    def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
+        super().__init__(cfg, weights, device)
+        c = cfg
+        dev = self.device
+
+        def w(name):
+            return weights[name].to(device=dev, dtype=torch.bfloat16).contiguous()
+
+        self.emb = torch.stack([w(f"embeddings.{k}.weight") for k in range(N_CB)]).contiguous()
+        assert self.emb.shape == (N_CB, VOCAB, c.d_model), self.emb.shape
+        heads = []
+        for k in range(N_CB):
+            h = w(f"heads.{k}.weight")
+            if h.shape[0] < VOCAB:      # pad_weight_ (utils.py:22-37): 1025 -> 1026 rows
+                h = torch.cat([h, h.new_zeros(VOCAB - h.shape[0], h.shape[1])])
+            heads.append(h)
+        self.heads = pack_weights(torch.cat(heads).contiguous(), _lib.stream_ptr(dev))  # [9*1026 -> 9280][D] packed
         self._ws = None
         torch.cuda.synchronize(dev)
 
@@ -209,48 +269,6 @@ class HipDecoder:
             self.release()
         except Exception:
             pass
-
-    def _kv(self, ws, layer):
-        return ws["kv"][layer, 0], ws["kv"][layer, 1]
-
-    # ------------------------------------------------------------------ transformer passes
-    def _layers(self, ws, M: int, R: int, S: int, prefill: bool, stream, skip):
-        """Run the 26 blocks on xn/x (rows = R*S). Leaves norm_f(x) in ws['xn']."""
-        c = self.cfg
-        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
-        Nqkv = (H + 2 * Hk) * hd
-        sp = ws["splits"] if not prefill else dict(qkv=1, o=1, fc2=1)
-        x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
-        scal = ws["scal"]
-        pos_dev = None if prefill else ptr(scal[1:2])
-        for i, L in enumerate(self.layers):
-            kc, vt = self._kv(ws, i)
-            call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
-            if prefill:
-                call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
-                     ptr(kc), ptr(vt), ws["smax"], None, self.rope_neox, skip, stream)
-                call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
-            elif self.fuse_qkv:
-                # in_proj epilogue fused into the attention launch (position = ctx - 1 = scal[1])
-                call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
-                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), self.rope_neox,
-                     skip, stream)
-            else:
-                call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
-                     ptr(kc), ptr(vt), ws["smax"], None, self.rope_neox, skip, stream)
-                call("zk_attn_decode", ptr(q), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1, ptr(scal[1:2]),
-                     ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), skip, stream)
-            call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip, stream)
-            call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D, ptr(x),
-                 ptr(xn), 0, skip, stream)
-            call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fd, D, 1, 1, None, ptr(h), skip, stream)
-            call("zk_gemm_bf16", ptr(h), Fd, ptr(L["fc2"]), M, D, Fd, sp["fc2"], 0, ptr(part), None, skip, stream)
-            if i + 1 < len(self.layers):
-                nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
-            else:
-                nw, nb = self.lnf_w, self.lnf_b
-            call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 0, skip,
-                 stream)
 
     def _heads(self, ws, R: int, S: int, stream, skip):
         """Heads GEMM on the last position of every row -> split-K slabs in ws['part']."""
