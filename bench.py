@@ -156,20 +156,21 @@ def attn_roofline(eng, ctx):
 
 
 def gemv_roofline(eng):
-    """B <= 8 (c2): the weight-streaming fc1 GEMV + SwiGLU epilogue (zk_gemm_bf16 -> k_gemv_rk, the
-    largest launch of the step), over the 26 layers' fc1 weights in turn (67 MB each: nothing stays
-    in L2/MALL between launches, as in the real step). Bytes = weights + activation + output."""
+    """B <= 8 (c2): the largest launch of the small-batch step -- fc1 with the norm2 LayerNorm
+    prologue and the SwiGLU epilogue (zk_gemv_fused -> k_gemv_f), launched as _layers_small
+    launches it, over the 26 layers' fc1 weights in turn (67 MB each: nothing stays in L2/MALL
+    between launches, as in the real step). Bytes = weights + residual rows + LN w/b + output."""
     from zonos_amd._lib import call, ptr
     ws, c = eng._ws, eng.cfg
     R, D, Fd = ws["R"], c.d_model, c.d_ff
 
     def launch(L):
-        return lambda st: call("zk_gemm_bf16", ptr(ws["xn"]), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, 1, None,
-                               ptr(ws["h"]), None, st)
+        return lambda st: call("zk_gemv_fused", ptr(ws["x"]), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, ptr(L["ln2_w"]),
+                               ptr(L["ln2_b"]), c.eps, None, ptr(ws["h"]), None, st)
     per = _time_launches([launch(L) for L in eng.layers if "fc1" in L], reps=4)
-    b = 2 * Fd * D * 2 + R * D * 2 + R * Fd * 2
-    return _roof(b, per, traffic=_pmc_traffic("k_gemv_rk", R=R, N=2 * Fd, K=D),
-                 kernel="k_gemv_rk (zk_gemm_bf16 fc1 + SwiGLU)", M=R, N=2 * Fd, K=D,
+    b = 2 * Fd * D * 2 + R * D * 2 + 2 * D * 2 + R * Fd * 2
+    return _roof(b, per, traffic=_pmc_traffic("k_gemv_f<1, true", R=R, N=2 * Fd, K=D),
+                 kernel="k_gemv_f<1,true,2> (zk_gemv_fused: norm2 LayerNorm + fc1 + SwiGLU)", M=R, N=2 * Fd, K=D,
                  layers="rotating over all layers' fc1 weights")
 
 
@@ -353,7 +354,7 @@ class GpuWorkload:
         ctx_mean = args.lc + args.prefix + 1 + n_dec // 2
         if args.model == "hybrid":
             roof = mamba_roofline(eng)
-        elif R <= 16:
+        elif eng._small(R):
             roof = gemv_roofline(eng)
         else:
             roof = attn_roofline(eng, ctx_mean)

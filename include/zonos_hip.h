@@ -93,6 +93,18 @@ int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, 
  * W is in the engine's fragment-packed layout (zk_pack_weights; rows padded to 64). */
 int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
                  float* Cpart, void* Cout, const int32_t* skip, void* stream);
+/* Small-batch (M <= 16) GEMV without split-K, for the B <= 8 decode layer (five launches per
+ * transformer block instead of seven; replaces the k_resid_ln launches of _torch.py:100-101):
+ *   ln_w/ln_b non-NULL: A holds the residual rows x (bf16, K = D = 2048) and every workgroup
+ *     applies nn.LayerNorm(eps) to them in its prologue (TransformerBlock.norm / norm2 /
+ *     backbone norm_f, _torch.py:78,100-101) before the product;
+ *   mode 0: Cf fp32 [M][N] = LN?(A) . W^T            (in_proj, heads: one "slab", nsplit 1)
+ *   mode 1: Cb bf16 [M][N/2] = SwiGLU(LN?(A) . W^T)  (fc1, interleaved rows as zk_gemm_bf16)
+ *   mode 2: Cb bf16 [M][N] += bf16(A . W^T), i.e. x = bf16(x + bf16(proj))   (out_proj, fc2)
+ * W fragment-packed (zk_pack_weights). K in {2048, 4096, 8192}; results depend on (N, K) only. */
+int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, int mode,
+                  const void* ln_w, const void* ln_b, float eps, float* Cf, void* Cb,
+                  const int32_t* skip, void* stream);
 /* fc1 weight [2F][D] (rows: F "y" then F "gate") -> interleaved groups of 8 y + 8 gate rows. */
 int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream);
 /* nn.Linear weight [N][K] bf16 -> fragment-packed [ceil64(N)/16][K/32][64][8] (rows >= N zero):

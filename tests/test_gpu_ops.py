@@ -302,3 +302,51 @@ def test_embed_codes():
     call("zk_embed_codes", ptr(idd), B, S, K, K * S, S, None, 0, ptr(ed), V, D, 2, ptr(out), S + 2, 2, None, None,
          1e-5, None, None, stream_ptr())
     assert torch.equal(out[:, 2:].cpu(), ref)          # bf16 sequential adds reproduced bit-exactly
+
+
+@pytest.mark.parametrize("M,N,K,mode,ln", [(2, 3072, 2048, 0, True), (16, 3072, 2048, 0, True), (5, 9234, 2048, 0, True),
+                                           (2, 2048, 2048, 2, False), (16, 2048, 8192, 2, False),
+                                           (1, 2048, 4096, 2, False), (2, 16384, 2048, 1, True),
+                                           (9, 16384, 2048, 1, True), (7, 4000, 2048, 0, False),
+                                           (3, 5000, 2048, 0, True), (4, 5000, 8192, 2, False)])
+def test_gemv_fused(M, N, K, mode, ln):
+    """Small-batch GEMV (zk_gemv_fused): LayerNorm prologue, fp32 / SwiGLU / residual epilogues,
+    half-tile, one-tile and two-tile layouts, against torch on the CPU at the same rounding points."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import pack_weights
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + mode)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(K, generator=g)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(K, generator=g)).to(torch.bfloat16)
+    s = stream_ptr()
+    a = F.layer_norm(x, (K,), w, b, 1e-5) if ln else x          # bf16 LayerNorm (fp32 inside), CPU
+    Wd = W.to(DEV)
+    if mode == 1:
+        Wp = torch.empty_like(Wd)
+        call("zk_permute_fc1", ptr(Wd), N // 2, K, ptr(Wp), s)
+        Wd = Wp
+    Wpk = pack_weights(Wd, s)
+    xd = x.to(DEV)
+    keep = (w.to(DEV), b.to(DEV))            # LayerNorm weight / bias (held alive for the call)
+    lw, lb = (ptr(keep[0]), ptr(keep[1])) if ln else (None, None)
+    if mode == 0:
+        out = torch.full((M, N), float("nan"), device=DEV)
+        call("zk_gemv_fused", ptr(xd), K, ptr(Wpk), M, N, K, 0, lw, lb, 1e-5, ptr(out), None, None, s)
+        ref = a.float() @ W.float().t()
+        # the LayerNorm'd activation differs by <= 1 bf16 ulp from torch's in a few elements
+        assert torch.allclose(out.cpu(), ref, atol=2e-2 if ln else 3e-3, rtol=1e-2), (out.cpu() - ref).abs().max()
+    elif mode == 1:
+        out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+        call("zk_gemv_fused", ptr(xd), K, ptr(Wpk), M, N, K, 1, lw, lb, 1e-5, None, ptr(out), None, s)
+        ry, rg = F.linear(a, W).chunk(2, dim=-1)
+        ref = ry * F.silu(rg)
+        err = (out.float().cpu() - ref.float()).abs()
+        assert err.max() < 0.06 and (err > 0).float().mean() < 0.06, err.max()
+    else:
+        res = torch.randn(M, N, generator=g).to(torch.bfloat16)
+        xr = res.to(DEV)
+        call("zk_gemv_fused", ptr(xd), K, ptr(Wpk), M, N, K, 2, None, None, 1e-5, None, ptr(xr), None, s)
+        ref = res + F.linear(x, W)                               # bf16 + bf16(proj), like _torch.py:100-101
+        err = (xr.float().cpu() - ref.float()).abs()
+        assert err.max() < 0.07 and (err > 0).float().mean() < 0.05, err.max()

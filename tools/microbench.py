@@ -147,6 +147,59 @@ def attn_one(R, H, Hk, hd, ctx, smax, kcs, vts, q, ms_, ncopy):
         print(f"attn ctx={ctx:5d} splits={ms_}: {us:8.1f} us  {b/1e6:7.1f} MB  {b / (us * 1e-6) / 1e9:7.0f} GB/s", flush=True)
 
 
+def gemv():
+    """Small-batch (M <= 16) decode projections: zk_gemv_fused (LN prologue / residual epilogue)
+    vs the split-K zk_gemm_bf16 + zk_resid_ln pair it replaces. Rotating weight copies."""
+    M = int(os.environ.get("ZK_MB_M", "2"))
+    D = 2048
+    x = torch.randn(M, 8192, device=dev).to(torch.bfloat16)
+    lw = torch.ones(D, device=dev, dtype=torch.bfloat16)
+    lb = torch.zeros(D, device=dev, dtype=torch.bfloat16)
+    res = torch.randn(M, D, device=dev).to(torch.bfloat16)
+    outf = torch.empty(M * 16384, device=dev)
+    outb = torch.empty(M * 16384, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(16 * M * 16384, device=dev)
+    xo, xn = torch.empty(M, D, device=dev, dtype=torch.bfloat16), torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    tot_new = tot_old = 0.0
+    shapes = (("qkv", 3072, 2048, 0, True), ("o", 2048, 2048, 2, False), ("fc1", 16384, 2048, 1, True),
+              ("fc2", 2048, 8192, 2, False), ("heads", 9234, 2048, 0, True))
+    if os.environ.get("ZK_MB_SHAPES"):      # "name:N:K:mode:ln,..." (extra tuning shapes)
+        shapes = [(a, int(b), int(c), int(d), e == "1") for a, b, c, d, e in
+                  (t.split(":") for t in os.environ["ZK_MB_SHAPES"].split(","))]
+    for name, N, K, mode, ln in shapes:
+        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
+        Npad = (N + 63) // 64 * 64
+        Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        it = [0]
+
+        def f():
+            W = Ws[it[0] % ncopy]
+            it[0] += 1
+            call("zk_gemv_fused", ptr(x), K, ptr(W), M, N, K, mode, ptr(lw) if ln else None, ptr(lb) if ln else None,
+                 1e-5, ptr(outf), ptr(res) if mode == 2 else ptr(outb), None, S)
+        us = timeit(f)
+        # the replaced pair: split-K GEMV (+ the k_resid_ln of a residual / LayerNorm edge)
+        gm = 1 if mode == 1 else _split_for(N, K, 2 * 8, 256 if name != "o" else 128)
+        gm = 1 if name == "heads" else gm
+
+        def g():
+            W = Ws[it[0] % ncopy]
+            it[0] += 1
+            call("zk_gemm_bf16", ptr(x), K, ptr(W), M, N, K, gm, mode if mode < 2 else 0, ptr(part), ptr(outb),
+                 None, S)
+            if mode == 2 or name == "fc1":
+                call("zk_resid_ln", ptr(part), gm, ptr(res), ptr(lw), ptr(lb), 1e-5, M, D, ptr(xo), ptr(xn), 0,
+                     None, S)
+        us_old = timeit(g)
+        tot_new += us
+        tot_old += us_old
+        gb = N * K * 2 / 1e9
+        print(f"gemv {name:6s} M={M} N={N:5d} K={K:5d}: fused {us:6.2f} us ({gb / (us * 1e-6):5.0f} GB/s)   "
+              f"split-K(+resid_ln) {us_old:6.2f} us", flush=True)
+        del Ws
+    print(f"gemv total per layer-ish: fused {tot_new:.1f} us, old {tot_old:.1f} us", flush=True)
+
+
 def dac():
     from zonos_amd import synthetic
     from zonos_amd.autoencoder import DacSpec, HipDacDecoder
@@ -164,6 +217,8 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
         gemm()
+    if what in ("gemv",):
+        gemv()
     if what in ("prefill", "all"):
         prefill()
     if what in ("ln", "all"):

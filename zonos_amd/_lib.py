@@ -46,6 +46,7 @@ _SIGS = {
     "zk_layernorm": [P, P, P, F, I, I, P, P],
     "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, I, P, P],
     "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
+    "zk_gemv_fused": [P, L, P, I, I, I, I, P, P, F, P, P, P, P],
     "zk_permute_fc1": [P, I, I, P, P],
     "zk_pack_weights": [P, I, I, P, P],
     "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, I, P, P],

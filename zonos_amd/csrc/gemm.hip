@@ -483,6 +483,241 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
     }
 }
 
+// ------------------------------------------------------------------ small-batch fused GEMV
+// M <= 16 (B <= 8 decode) without split-K, so a transformer layer is five launches:
+//   [LN1 prologue + in_proj] -> attention -> [out_proj + residual] -> [LN2 prologue + fc1 +
+//   SwiGLU] -> [fc2 + residual]   (and [norm_f prologue + heads]).
+// The M <= 16 activation is tiny, so instead of a separate k_resid_ln launch per residual
+// every workgroup of the consuming GEMV recomputes the LayerNorm of the (<= 16) input rows
+// into LDS; its weight prefetch is issued right behind the row loads, so the prologue runs
+// under the weight stream's first round trip. The producing GEMV adds its bf16 output to the
+// residual row in its epilogue (x = bf16(x + bf16(A.W^T)), _torch.py:100-101) -- no fp32
+// split-K slabs leave the workgroup: the 4 waves split K and are summed through LDS in a
+// fixed order (q0 + q1 + q2 + q3), so results depend on (N, K) only, not on M <= 16.
+// Layouts: NTW 16-column tiles per workgroup; HALF: 8 columns (half a packed tile: the lanes
+// of the other half load nothing, the tile's other 8 columns belong to the neighbouring
+// workgroup -- 4 of the 8 128-B lines of every 1 KB fragment each) so N = 2048 still gives
+// 256 workgroups.
+// mode 0: fp32 Cf[M][N]; mode 1: SwiGLU -> bf16 Cb[M][N/2]; mode 2: residual, Cb = x bf16 [M][N].
+ZK_DEV void opaque(uint4& v) {
+    u32x4 t = __builtin_bit_cast(u32x4, v);
+    asm volatile("" : "+v"(t));
+    v = __builtin_bit_cast(uint4, t);
+}
+
+// DPP row rotation (within each 16-lane row) of a 32-bit value
+template <int R>
+ZK_DEV float row_ror(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xF, 0xF, false));
+}
+template <int R>
+ZK_DEV uint4 row_ror4(uint4 v) {
+    uint4 o;
+    o.x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x120 + R, 0xF, 0xF, false);
+    o.y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x120 + R, 0xF, 0xF, false);
+    o.z = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x120 + R, 0xF, 0xF, false);
+    o.w = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x120 + R, 0xF, 0xF, false);
+    return o;
+}
+// wave64 sum without LDS permutes: rotations inside each 16-lane row, then the 4 row sums
+// (read lanes 0, 16, 32, 48) added in row order. Every lane gets the same value.
+ZK_DEV float wave_sum_dpp(float v) {
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    v += row_ror<2>(v);
+    v += row_ror<1>(v);
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return ((r0 + r1) + r2) + r3;
+}
+
+constexpr int GF_XS = 2048 + 8;    // LDS row stride (bf16) of the LayerNorm'd rows (K = 2048)
+
+// NW waves split K (wave w: K range w/NW); KS k-steps of 32 per wave; PF loads in flight.
+// HALF: every weight load instruction fetches 1 KB of this workgroup's 8 columns by pairing
+// k-steps -- the owning lanes read k-step 2j of the packed fragment, the other half's lanes
+// read k-step 2j+1 at their neighbour's position (lane ^ 8); a DPP row rotation by 8 then moves
+// the k-step 2j+1 values to the owning lanes for the second MFMA. The other half's output
+// columns are garbage and never stored.
+template <int MODE, bool LN, int NTW, bool HALF, int NW, int KS, int PF>
+__global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict__ A, long lda,
+                                                       const bf16_t* __restrict__ W, int M, int N, int K,
+                                                       const bf16_t* __restrict__ lnw, const bf16_t* __restrict__ lnb,
+                                                       float eps, float* __restrict__ Cf, bf16_t* __restrict__ Cb,
+                                                       const int32_t* skip) {
+    static_assert(!HALF || NTW == 1, "HALF is one half tile");
+    static_assert(!LN || KS * NW * 32 == 2048, "LN prologue: K = 2048");
+    static_assert(NTW <= NW, "one finishing wave per tile");
+    constexpr int KPL = HALF ? 2 : 1;                                // k-steps per weight load
+    constexpr int NL = KS / KPL;                                     // weight loads per wave and tile
+    static_assert(NL * KPL == KS, "HALF pairs k-steps");
+    constexpr int MR = 16 / NW;                                      // LN rows per wave
+    __shared__ __attribute__((aligned(16))) uint4 xs[LN ? 16 * GF_XS / 8 : 1];
+    __shared__ __attribute__((aligned(16))) f32x4 red[NW][NTW][64];
+    if (skip && *skip) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ln = lane & 15, lg = lane >> 4;
+    const int nt0 = HALF ? (blockIdx.x >> 1) : blockIdx.x * NTW;    // first 16-column tile
+    const int half = HALF ? (blockIdx.x & 1) : 0;
+    const bool wl = !HALF || ((ln >> 3) == half);                   // this lane's column is ours
+    const int ntiles = (N + 63) / 64 * 4;                           // packed rows padded to 64
+    const int kbeg = w * (K / NW);
+    const int mrow = min(ln, M - 1);
+
+    // Loads that do not depend on the weight stream go FIRST: vmcnt retires in issue order, so
+    // the prologue (LN rows) / epilogue (residual) data must be older than the weight prefetch
+    // to be waited for without draining it. The empty asm with a memory clobber + sched_barrier
+    // keep the compiler from moving these loads behind the prefetch.
+    constexpr int NJ = LN ? 4 : 1;                                   // 16-B chunks per lane per row
+    uint4 xv[LN ? MR : 1][NJ], wv[NJ], bv[NJ];
+    if constexpr (LN) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            wv[j] = *reinterpret_cast<const uint4*>(lnw + lane * 8 + j * 512);
+            bv[j] = *reinterpret_cast<const uint4*>(lnb + lane * 8 + j * 512);
+        }
+#pragma unroll
+        for (int rr = 0; rr < MR; ++rr)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                xv[rr][j] = *reinterpret_cast<const uint4*>(A + (size_t)min(w + NW * rr, M - 1) * lda + lane * 8 + j * 512);
+    }
+    bf16_t rv[4] = {0, 0, 0, 0};                                     // residual x of the epilogue
+    const int t = w;                                                 // wave w finishes tile w
+    const int n_out = (nt0 + t) * 16 + ln;
+    if constexpr (MODE == 2) {
+        if (t < NTW && wl && n_out < N) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rv[i] = Cb[(size_t)min(lg * 4 + i, M - 1) * N + n_out];
+        }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    const int lsrc = wl ? lane * 8 : 512 + (lane ^ 8) * 8;          // HALF: k-step 2j+1 for the other half
+    const bf16_t* wp[NTW];
+#pragma unroll
+    for (int tt = 0; tt < NTW; ++tt)
+        wp[tt] = W + ((size_t)min(nt0 + tt, ntiles - 1) * (K >> 5) + (kbeg >> 5)) * 512 + lsrc;
+    const bf16_t* ap = A + (size_t)mrow * lda + kbeg + lg * 8;
+    constexpr int U = PF + 1;
+    uint4 wr[U][NTW], ar[U][KPL];
+    auto issue = [&](int ls, int slot) {
+#pragma unroll
+        for (int tt = 0; tt < NTW; ++tt) wr[slot][tt] = ldg_w<true>(wp[tt] + ls * 512 * KPL);
+        if constexpr (!LN) {
+#pragma unroll
+            for (int q = 0; q < KPL; ++q) ar[slot][q] = *reinterpret_cast<const uint4*>(ap + (ls * KPL + q) * 32);
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (p < NL) issue(p, p);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    if constexpr (LN) {
+        // the row values pass through an empty asm here, so no arithmetic on them (and therefore
+        // no wait for them) can be hoisted above the weight prefetch
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            opaque(wv[j]);
+            opaque(bv[j]);
+#pragma unroll
+            for (int rr = 0; rr < MR; ++rr) opaque(xv[rr][j]);
+        }
+        // LayerNorm of each row by one wave (nn.LayerNorm: two-pass fp32 mean / var,
+        // y = (x - mean) * rstd * w + b rounded to bf16 -- the arithmetic of ln_row_pre)
+        bf16_t* xsb = reinterpret_cast<bf16_t*>(xs);
+#pragma unroll
+        for (int rr = 0; rr < MR; ++rr) {       // unconditional (clamped rows): the loads above
+            const int m = w + NW * rr;            // stay where they are, only the store is masked
+            float xf[NJ * 8];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) unpack8(xv[rr][j], xf + 8 * j);
+            float s = 0.f;
+#pragma unroll
+            for (int e = 0; e < NJ * 8; ++e) s += xf[e];
+            const float mean = wave_sum_dpp(s) / (float)K;
+            float v = 0.f;
+#pragma unroll
+            for (int e = 0; e < NJ * 8; ++e) { const float d = xf[e] - mean; v += d * d; }
+            const float var = wave_sum_dpp(v) / (float)K;
+            const float rstd = 1.0f / sqrtf(var + eps);
+            const float nb = -rstd * mean;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                float wf[8], bf[8], o[8];
+                unpack8(wv[j], wf);
+                unpack8(bv[j], bf);
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(xf[8 * j + e], rstd), nb), wf[e]), bf[e]);
+                if (m < M) *reinterpret_cast<uint4*>(xsb + m * GF_XS + lane * 8 + j * 512) = pack8(o);
+            }
+        }
+        __syncthreads();
+    }
+
+    f32x4 acc[NTW];
+#pragma unroll
+    for (int tt = 0; tt < NTW; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* xrow = reinterpret_cast<const bf16_t*>(xs) + mrow * GF_XS + kbeg + lg * 8;
+#pragma unroll
+    for (int ls = 0; ls < NL; ++ls) {
+        if (ls + PF < NL) issue(ls + PF, (ls + PF) % U);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < KPL; ++q) {
+            uint4 a;
+            if constexpr (LN) a = *reinterpret_cast<const uint4*>(xrow + (ls * KPL + q) * 32);
+            else a = ar[ls % U][q];
+#pragma unroll
+            for (int tt = 0; tt < NTW; ++tt) {
+                const uint4 b = q == 0 ? wr[ls % U][tt] : row_ror4<8>(wr[ls % U][tt]);
+                acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(b), acc[tt], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int tt = 0; tt < NTW; ++tt) red[w][tt][lane] = acc[tt];
+    __syncthreads();
+    if (t >= NTW) return;
+    f32x4 sum = red[0][t][lane];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {
+        const f32x4 o = red[q][t][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sum[i] = sum[i] + o[i];
+    }
+    if (MODE == 1) {
+        const int F = N / 2;
+        const int f = (nt0 + t) * 8 + (ln & 7);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float mine = round_bf(sum[i]);
+            const float other = __shfl_xor(mine, 8, 64);
+            const int m = lg * 4 + i;
+            if (ln < 8 && m < M && f < F) {
+                const float sl = round_bf(other / (1.0f + expf(-other)));
+                Cb[(size_t)m * F + f] = f2bf(mine * sl);
+            }
+        }
+        return;
+    }
+    if (!wl || n_out >= N) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = lg * 4 + i;
+        if (m >= M) continue;
+        if (MODE == 0) Cf[(size_t)m * N + n_out] = sum[i];
+        else Cb[(size_t)m * N + n_out] = f2bf(bf2f(rv[i]) + round_bf(sum[i]));
+    }
+}
+
 // nn.Linear [N][K] -> fragment-packed [Npad/16][K/32][64][8] (rows >= N zero)
 __global__ void k_pack_w(const bf16_t* __restrict__ w, int N, int K, int Npad, bf16_t* __restrict__ out) {
     const size_t total = (size_t)Npad / 16 * (K / 32) * 64;      // 16-byte pieces
@@ -653,6 +888,77 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     }
 #undef ZK_GEMM_LAUNCH
     ZK_CHECK_LAUNCH("zk_gemm_bf16");
+    return 0;
+}
+
+extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, int mode,
+                             const void* ln_w, const void* ln_b, float eps, float* Cf, void* Cb,
+                             const int32_t* skip_flag, void* stream) {
+    ZK_REQUIRE(M >= 1 && M <= 16 && N > 0, "zk_gemv_fused: M=%d (1..16) N=%d", M, N);
+    ZK_REQUIRE(K == 2048 || K == 4096 || K == 8192, "zk_gemv_fused: K=%d (2048, 4096 or 8192)", K);
+    ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemv_fused: lda=%ld", lda);
+    ZK_REQUIRE(mode >= 0 && mode <= 2, "zk_gemv_fused: mode %d", mode);
+    ZK_REQUIRE(mode != 1 || N % 16 == 0, "zk_gemv_fused: SwiGLU needs N %% 16 == 0");
+    ZK_REQUIRE((ln_w == nullptr) == (ln_b == nullptr), "zk_gemv_fused: LN needs both w and b");
+    ZK_REQUIRE(ln_w == nullptr || K == 2048, "zk_gemv_fused: LN prologue needs K = 2048 (K=%d)", K);
+    ZK_REQUIRE(mode == 0 ? Cf != nullptr : Cb != nullptr, "zk_gemv_fused: missing output");
+    const int tiles = (N + 15) / 16;
+    // >= 256 workgroups: half tiles below 256 tiles (out_proj / fc2: N = 2048), pairs of tiles
+    // from 512 (fc1, heads). With the LayerNorm prologue one tile per workgroup even below 256
+    // tiles (in_proj, N = 3072: 192 workgroups, 6.5 vs 7.5 us with half tiles at B = 1 --
+    // the prologue's latency, not the weight stream, sets its time; tools/gemv_probe.sh)
+    int lay = (mode != 1 && tiles < 256 && !ln_w) ? 0 : (tiles >= 512 ? 2 : 1);
+    static const int lay_force = [] {       // tuning knob (not used by default): 0 half, 1 one, 2 two tiles
+        const char* e = getenv("ZK_GF_LAYOUT");
+        return e ? atoi(e) : -1;
+    }();
+    if (lay_force >= 0 && !(lay_force == 0 && mode == 1)) lay = lay_force;
+    const int grid = lay == 0 ? 2 * tiles : (lay == 2 ? (tiles + 1) / 2 : tiles);
+    const bool ln = ln_w != nullptr;
+    (void)ln;
+    bool handled = false;
+    // tuning knobs (compile-time, build_variant): waves per workgroup, k-steps in flight per wave
+#ifndef ZK_GF_NW
+#define ZK_GF_NW 4
+#endif
+#ifndef ZK_GF_NWH
+#define ZK_GF_NWH 8
+#endif
+#ifndef ZK_GF_PF
+#define ZK_GF_PF 8
+#endif
+#define ZK_GF(MODE_, LN_, NTW_, HALF_, NW_, KSW_)                                                            \
+    do {                                                                                                      \
+        constexpr int KS_ = (KSW_) / (NW_);                                                                   \
+        constexpr int NL_ = HALF_ ? KS_ / 2 : KS_;                                                            \
+        hipLaunchKernelGGL((k_gemv_f<MODE_, LN_, NTW_, HALF_, NW_, KS_, (NL_ < ZK_GF_PF ? NL_ : ZK_GF_PF)>),  \
+                           dim3(grid), dim3(64 * (NW_)), 0, (hipStream_t)stream, (const bf16_t*)A, lda,        \
+                           (const bf16_t*)W, M, N, K, (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, Cf,        \
+                           (bf16_t*)Cb, skip_flag);                                                            \
+        handled = true;                                                                                       \
+    } while (0)
+#define ZK_GF_LAY(MODE_, LN_, KSW_)                                     \
+    do {                                                                \
+        if (lay == 0) ZK_GF(MODE_, LN_, 1, true, ZK_GF_NWH, KSW_);      \
+        else if (lay == 1) ZK_GF(MODE_, LN_, 1, false, ZK_GF_NW, KSW_); \
+        else ZK_GF(MODE_, LN_, 2, false, ZK_GF_NW, KSW_);               \
+    } while (0)
+#define ZK_GF_MODE(LN_, KSW_)                       \
+    do {                                            \
+        if (mode == 0) ZK_GF_LAY(0, LN_, KSW_);     \
+        else if (mode == 1) ZK_GF_LAY(1, LN_, KSW_); \
+        else ZK_GF_LAY(2, LN_, KSW_);               \
+    } while (0)
+    // KSW = K / 32: k-steps of the whole workgroup
+    if (ln) ZK_GF_MODE(true, 64);
+    else if (K == 2048) ZK_GF_MODE(false, 64);
+    else if (K == 4096) ZK_GF_MODE(false, 128);
+    else ZK_GF_MODE(false, 256);
+#undef ZK_GF_MODE
+#undef ZK_GF_LAY
+#undef ZK_GF
+    ZK_REQUIRE(handled, "zk_gemv_fused: no kernel for K=%d", K);
+    ZK_CHECK_LAUNCH("zk_gemv_fused");
     return 0;
 }
 

@@ -140,6 +140,28 @@ class HipBackbone:
         self.lnf_b = w("norm_f.bias")
         self.freqs = rope_table(16384, c.head_dim).to(dev)
 
+    def _layers_small(self, ws, R: int, stream, skip):
+        """Decode step of the 26 blocks for R <= 16 rows (B <= 8), five launches per block:
+        [norm -> in_proj] -> attention (RoPE, KV write) -> [out_proj -> x += .] ->
+        [norm2 -> fc1 -> SwiGLU] -> [fc2 -> x += .] (_torch.py:99-102, 117-152). Leaves the
+        residual stream in ws['x'] (norm_f runs in the heads GEMV's prologue)."""
+        c = self.cfg
+        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+        Nqkv = (H + 2 * Hk) * hd
+        x, y, h, part, scal = ws["x"], ws["y"], ws["h"], ws["part"], ws["scal"]
+        for i, L in enumerate(self.layers):
+            kc, vt = self._kv(ws, i)
+            call("zk_gemv_fused", ptr(x), D, ptr(L["wqkv"]), R, Nqkv, D, 0, ptr(L["ln1_w"]), ptr(L["ln1_b"]), c.eps,
+                 ptr(part), None, skip, stream)
+            call("zk_attn_decode_qkv", ptr(part), 1, ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1,
+                 ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), self.rope_neox, skip, stream)
+            call("zk_gemv_fused", ptr(y), H * hd, ptr(L["wo"]), R, D, H * hd, 2, None, None, c.eps, None, ptr(x),
+                 skip, stream)
+            call("zk_gemv_fused", ptr(x), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, ptr(L["ln2_w"]), ptr(L["ln2_b"]),
+                 c.eps, None, ptr(h), skip, stream)
+            call("zk_gemv_fused", ptr(h), Fd, ptr(L["fc2"]), R, D, Fd, 2, None, None, c.eps, None, ptr(x), skip,
+                 stream)
+
     def _kv(self, ws, layer):
         if "kv_layers" in ws:            # caches handed out per layer (backbone plugin)
             kv = ws["kv_layers"][layer]
@@ -188,6 +210,10 @@ class HipBackbone:
 
 class HipDecoder(HipBackbone):
     """Owns device weights in engine layout and runs generate() on the GPU."""
+
+    # B <= 8 decode (R <= 16 rows) runs each block as five launches (zk_gemv_fused: LayerNorm
+    # prologues, residual epilogues, no split-K slabs) instead of seven; ZK_SMALL=0 disables it
+    small_batch_path = os.environ.get("ZK_SMALL", "1") != "0"
 
     def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
         super().__init__(cfg, weights, device)
@@ -288,15 +314,25 @@ class HipDecoder(HipBackbone):
         scal = ws["scal"]
         skip = ptr(scal[3:4])
         L0 = self.layers[0]
+        small = self._small(R)      # small path: layer 0's LayerNorm runs in the in_proj prologue
         call("zk_embed_codes", ptr(ws["delayed"]), B, 1, N_CB, ws["Ld"] * N_CB, ws["Ld"], ptr(scal[0:1]), -1,
-             ptr(self.emb), VOCAB, c.d_model, 2, ptr(ws["x"]), 1, 0, ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps,
-             ptr(ws["xn"]), skip, stream)
-        self._layers(ws, R, R, 1, False, stream, skip)
-        self._heads(ws, R, 1, stream, skip)
+             ptr(self.emb), VOCAB, c.d_model, 2, ptr(ws["x"]), 1, 0, None if small else ptr(L0["ln1_w"]),
+             None if small else ptr(L0["ln1_b"]), c.eps, None if small else ptr(ws["xn"]), skip, stream)
+        if self._small(R):
+            self._layers_small(ws, R, stream, skip)
+            # heads with the final LayerNorm (norm_f) as the GEMV prologue: one fp32 slab
+            call("zk_gemv_fused", ptr(ws["x"]), c.d_model, ptr(self.heads), R, N_CB * VOCAB, c.d_model, 0,
+                 ptr(self.lnf_w), ptr(self.lnf_b), c.eps, ptr(ws["part"]), None, skip, stream)
+        else:
+            self._layers(ws, R, R, 1, False, stream, skip)
+            self._heads(ws, R, 1, stream, skip)
         nsp = ws["splits"]["heads"]
         call("zk_sample_heads", ptr(ws["part"]), nsp, C_ref(st), C_ref(sp), 0, 0, ptr(ws["dbg"]), stream)
         call("zk_sample_heads", ptr(ws["part"]), nsp, C_ref(st), C_ref(sp), 0, 1, None, stream)
         call("zk_eos_step", C_ref(st), 0, 0, stream)
+
+    def _small(self, R: int) -> bool:
+        return self.small_batch_path and R <= 16 and self.cfg.d_model == 2048
 
     # ------------------------------------------------------------------ generate
     @torch.inference_mode()

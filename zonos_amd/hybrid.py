@@ -95,6 +95,8 @@ def rotary_table(seq_len: int, dim: int, base: float = 10000.0) -> torch.Tensor:
 class HybridDecoder(HipDecoder):
     """generate() for the hybrid backbone (the layer loop and state differ from HipDecoder)."""
 
+    small_batch_path = False      # the hybrid block sequence has its own _layers (prenorm add + norm)
+
     def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda"):
         _lib.load()
         if cfg.d_conv != 4 or cfg.ngroups != 1:
