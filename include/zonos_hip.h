@@ -150,6 +150,15 @@ int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const float* freqs, v
                        const int32_t* ctx_dev, float* work, int nsplit, void* out, int rope_neox,
                        const int32_t* skip, void* stream);
 
+/* zk_attn_decode_qkv with the split-KV partials merged inside the launch (no k_attn_combine):
+ * counters = uint32 [R][Hkv], zeroed once before the first launch (each launch adds nsplit per
+ * (row, kv head); the workgroup drawing the last ticket merges). nsplit == 1 or counters == NULL
+ * is zk_attn_decode_qkv. Same results as the two-launch form, bit for bit. */
+int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
+                          void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
+                          const int32_t* ctx_dev, float* work, int nsplit, uint32_t* counters, void* out,
+                          int rope_neox, const int32_t* skip, void* stream);
+
 /* ------------------------------------------------------------------ graphs and timing
  * The decode step is captured once into a hipGraph and replayed (the reference runs the
  * transformer step eagerly: model.py:138-142, 220-222). */

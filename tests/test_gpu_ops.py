@@ -350,3 +350,34 @@ def test_gemv_fused(M, N, K, mode, ln):
         ref = res + F.linear(x, W)                               # bf16 + bf16(proj), like _torch.py:100-101
         err = (xr.float().cpu() - ref.float()).abs()
         assert err.max() < 0.07 and (err > 0).float().mean() < 0.05, err.max()
+
+
+@pytest.mark.parametrize("R,ctx,nsplit", [(2, 600, 5), (2, 1000, 8), (16, 300, 3), (4, 129, 2)])
+def test_attention_split_combine_in_launch(R, ctx, nsplit):
+    """zk_attn_decode_qkv_sc (split partials merged inside the launch by the last workgroup of
+    each (row, kv head)) == zk_attn_decode_qkv + k_attn_combine, bit for bit, over repeated
+    launches (the ticket counters carry over from launch to launch)."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import rope_table
+    H, Hk, hd = 16, 4, 128
+    smax = ((ctx + 255) // 256) * 256
+    g = torch.Generator(device="cpu").manual_seed(ctx)
+    kc = torch.randn(R * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    vt = torch.randn(R * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    freqs = rope_table(16384, hd).to(DEV)
+    work = torch.empty(R * Hk * nsplit * (8 + 4 * hd), device=DEV)
+    cnt = torch.zeros(R * Hk, dtype=torch.int32, device=DEV)
+    s = stream_ptr()
+    for rep in range(3):
+        part = (torch.randn(R * (H + 2 * Hk) * hd, generator=g) * 0.5).to(DEV)
+        kc2, vt2 = kc.clone(), vt.clone()
+        ref = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
+        call("zk_attn_decode_qkv", ptr(part), 1, ptr(freqs), ptr(kc2), ptr(vt2), R, H, Hk, hd, smax, ctx + rep, None,
+             ptr(work), nsplit, ptr(ref), 0, None, s)
+        out = torch.full((R, H * hd), float("nan"), dtype=torch.bfloat16, device=DEV)
+        call("zk_attn_decode_qkv_sc", ptr(part), 1, ptr(freqs), ptr(kc), ptr(vt), R, H, Hk, hd, smax, ctx + rep, None,
+             ptr(work), nsplit, ptr(cnt), ptr(out), 0, None, s)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (rep, (out.float() - ref.float()).abs().max())
+        assert torch.equal(kc, kc2) and torch.equal(vt, vt2)
+    assert bool((cnt.cpu() % nsplit == 0).all()) and int(cnt.cpu()[0]) == 3 * nsplit

@@ -131,6 +131,55 @@ def attn():
         print(f"qkv_rope alone ctx={ctx:5d}: {us:8.1f} us", flush=True)
 
 
+def attn_small():
+    """B = 1 decode attention (R = 2 rows) with the fused in_proj epilogue: one workgroup per
+    (row, kv head) vs key splits merged by k_attn_combine (second launch) or in the launch
+    (zk_attn_decode_qkv_sc). 26 rotating caches, as the 26 layers of a step."""
+    from zonos_amd.engine import rope_table
+    R, H, Hk, hd = int(os.environ.get("ZK_MB_R", "2")), 16, 4, 128
+    smax = 1280
+    nl = 26
+    kcs = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(nl)]
+    vts = [torch.randn(R * Hk * smax * hd, device=dev).to(torch.bfloat16) for _ in range(nl)]
+    part = torch.randn(R * (H + 2 * Hk) * hd, device=dev) * 0.1
+    freqs = rope_table(16384, hd).to(dev)
+    out = torch.empty(R, H * hd, dtype=torch.bfloat16, device=dev)
+    cnt = torch.zeros(R * Hk, dtype=torch.int32, device=dev)
+    q = torch.randn(R, H * hd, device=dev).to(torch.bfloat16)
+    for ctx in (1, 300, 600):
+        it = [0]
+
+        def fu():
+            i = it[0] % nl
+            it[0] += 1
+            call("zk_attn_decode", ptr(q), ptr(kcs[i]), ptr(vts[i]), R, H, Hk, hd, smax, ctx, None, None, 1, ptr(out),
+                 None, S)
+        print(f"attn R={R} ctx={ctx:5d} unfused (q given), unsplit: {timeit(fu, reps=104, warm=26):6.2f} us", flush=True)
+
+        def fr():
+            call("zk_qkv_rope", ptr(part), 1, R, 1, H, Hk, hd, ptr(freqs), ctx - 1, None, ptr(q), ptr(kcs[0]),
+                 ptr(vts[0]), smax, None, 0, None, S)
+        print(f"qkv_rope alone R={R}: {timeit(fr, reps=104, warm=26):6.2f} us", flush=True)
+    for ctx in (ENV_CTX if (ENV_CTX := [int(c) for c in os.environ.get("ZK_MB_CTX", "").split(",") if c]) else
+                (1, 300, 600, 1000)):
+        for ns in (1, 2, 4, 8):
+            work = torch.empty(R * Hk * ns * (8 + 4 * hd), device=dev)
+            for sc in ((False, True) if ns > 1 else (False,)):
+                it = [0]
+
+                def f():
+                    i = it[0] % nl
+                    it[0] += 1
+                    if sc:
+                        call("zk_attn_decode_qkv_sc", ptr(part), 1, ptr(freqs), ptr(kcs[i]), ptr(vts[i]), R, H, Hk,
+                             hd, smax, ctx, None, ptr(work), ns, ptr(cnt), ptr(out), 0, None, S)
+                    else:
+                        call("zk_attn_decode_qkv", ptr(part), 1, ptr(freqs), ptr(kcs[i]), ptr(vts[i]), R, H, Hk, hd,
+                             smax, ctx, None, ptr(work), ns, ptr(out), 0, None, S)
+                us = timeit(f, reps=104, warm=26)
+                print(f"attn R={R} ctx={ctx:5d} splits={ns:2d} {'in-launch combine' if sc else 'combine launch  ' if ns > 1 else 'unsplit         '}: {us:6.2f} us", flush=True)
+
+
 def attn_one(R, H, Hk, hd, ctx, smax, kcs, vts, q, ms_, ncopy):
     if True:
         work = torch.empty(R * Hk * ms_ * (8 + 4 * hd), device=dev)
@@ -217,6 +266,8 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
         gemm()
+    if what in ("attn_small",):
+        attn_small()
     if what in ("gemv",):
         gemv()
     if what in ("prefill", "all"):

@@ -426,11 +426,17 @@ ZK_DEV void patch_kv(KVFrag& f, const uint32_t* s_kn, const uint16_t* s_vn, int 
 // reduces the split-K slabs of its own 4 query heads + 1 KV head (768 columns), applies RoPE,
 // keeps q in LDS and (the split that owns the newest key) stores the new K / V^T entries
 // before the key loop reads them. One launch per layer instead of two.
-template <bool FUSED, bool NEOX, bool KVNT>
+// COMB (nsplit > 1): the splits of one (row, kv head) combine in this launch instead of in
+// k_attn_combine -- each workgroup publishes its partial (m, l, O) (stores drained, agent-scope
+// release) and takes a ticket on cnt[row][kv head]; the workgroup drawing the last ticket of the
+// launch (tickets are monotonic: the count is a multiple of nsplit before every launch) acquires
+// and merges all nsplit partials exactly as k_attn_combine does. Saves the combine launch.
+template <bool FUSED, bool NEOX, bool KVNT, bool COMB = false>
 __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H,
                                                         int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
                                                         float* work, float scale, bf16_t* out, const int32_t* skip,
-                                                        const float* part, int gsplit, const float* freqs) {
+                                                        const float* part, int gsplit, const float* freqs,
+                                                        uint32_t* cnt = nullptr) {
     constexpr int HD = 128;
     __shared__ float s_m[4][16];
     __shared__ float s_l[4][16];
@@ -438,6 +444,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     __shared__ __attribute__((aligned(16))) uint32_t s_q[AT_G][HD / 2];
     __shared__ __attribute__((aligned(16))) uint32_t s_kn[HD / 2];   // new key (post-RoPE), bf16 pairs
     __shared__ uint16_t s_vn[HD];                                    // new value
+    __shared__ int s_last;                                           // COMB: this workgroup merges
     if (skip && *skip) return;
     const int split = blockIdx.x, nsplit = gridDim.x, g = blockIdx.y, r = blockIdx.z;
     const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
@@ -590,6 +597,41 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
         for (int k = 0; k < 4; ++k) L += (s_m[k][h] == -INFINITY) ? 0.f : s_l[k][h] * __expf(s_m[k][h] - Mh);
         wp[h] = Mh;
         wp[AT_G + h] = L;
+    }
+    if constexpr (COMB) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // keep the fence's wait (ROCm 7.2)
+            const uint32_t old = __hip_atomic_fetch_add(cnt + (size_t)r * Hkv + g, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            s_last = ((old + 1) % (uint32_t)nsplit) == 0;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        const float* base = work + ((size_t)r * Hkv + g) * nsplit * AT_STR;
+        for (int i = threadIdx.x; i < G * HD / 2; i += 256) {       // k_attn_combine's arithmetic
+            const int j = i / (HD / 2), d = (i % (HD / 2)) * 2;
+            float M = -INFINITY;
+            for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, base[sp * AT_STR + j]);
+            float L = 0.f, o0 = 0.f, o1 = 0.f;
+            for (int sp = 0; sp < nsplit; ++sp) {
+                const float* p = base + sp * AT_STR;
+                const float c = (p[j] == -INFINITY) ? 0.f : __expf(p[j] - M);
+                L += p[AT_G + j] * c;
+                o0 += p[2 * AT_G + j * HD + d] * c;
+                o1 += p[2 * AT_G + j * HD + d + 1] * c;
+            }
+            const float inv = 1.0f / L;
+            *reinterpret_cast<uint32_t*>(out + (size_t)r * H * HD + (size_t)(g * G + j) * HD + d) =
+                pack2(o0 * inv, o1 * inv);
+        }
     }
 }
 
@@ -792,7 +834,7 @@ extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt
     auto kern = kvnt ? k_attn_decode<false, false, true> : k_attn_decode<false, false, false>;
     hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work,
-                       scale, (bf16_t*)out, skip, nullptr, 0, nullptr);
+                       scale, (bf16_t*)out, skip, nullptr, 0, nullptr, nullptr);
     ZK_CHECK_LAUNCH("zk_attn_decode");
     if (nsplit > 1) {
         hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, nsplit,
@@ -825,13 +867,39 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
                           : (kvnt ? k_attn_decode<true, false, true> : k_attn_decode<true, false, false>);
     hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq, (bf16_t*)k_cache,
                        (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out, skip, part,
-                       gemm_nsplit, freqs);
+                       gemm_nsplit, freqs, nullptr);
     ZK_CHECK_LAUNCH("zk_attn_decode_qkv");
     if (nsplit > 1) {
         hipLaunchKernelGGL(k_attn_combine, dim3(H, R), dim3(64), 0, (hipStream_t)stream, work, H, Hkv, nsplit,
                            (bf16_t*)out, skip);
         ZK_CHECK_LAUNCH("zk_attn_combine");
     }
+    return 0;
+}
+
+extern "C" int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
+                                     void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
+                                     const int32_t* ctx_dev, float* work, int nsplit, uint32_t* counters, void* out,
+                                     int rope_neox, const int32_t* skip, void* stream) {
+    if (nsplit == 1 || counters == nullptr)
+        return zk_attn_decode_qkv(part, gemm_nsplit, freqs, k_cache, vt_cache, R, H, Hkv, hd, Smax, ctx0, ctx_dev,
+                                  work, nsplit, out, rope_neox, skip, stream);
+    ZK_REQUIRE(hd == 128, "zk_attn_decode_qkv_sc: head_dim %d unsupported (128 only)", hd);
+    ZK_REQUIRE(H % Hkv == 0 && H / Hkv <= AT_G, "zk_attn_decode_qkv_sc: GQA group %d > %d", H / Hkv, AT_G);
+    ZK_REQUIRE(Smax % AT_KB == 0, "zk_attn_decode_qkv_sc: Smax=%d must be a multiple of %d", Smax, AT_KB);
+    ZK_REQUIRE(nsplit >= 1 && nsplit <= Smax / AT_KB, "zk_attn_decode_qkv_sc: nsplit=%d out of [1, %d]", nsplit,
+               Smax / AT_KB);
+    ZK_REQUIRE(work != nullptr, "zk_attn_decode_qkv_sc: nsplit > 1 needs the work buffer");
+    ZK_REQUIRE(part != nullptr && freqs != nullptr && gemm_nsplit >= 1 && gemm_nsplit <= AT_MAXGS,
+               "zk_attn_decode_qkv_sc: bad arguments (gemm_nsplit=%d, max %d)", gemm_nsplit, AT_MAXGS);
+    const float scale = 1.0f / sqrtf((float)hd);
+    const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
+    auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true, true> : k_attn_decode<true, true, false, true>)
+                          : (kvnt ? k_attn_decode<true, false, true, true> : k_attn_decode<true, false, false, true>);
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
+                       (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out, skip, part,
+                       gemm_nsplit, freqs, counters);
+    ZK_CHECK_LAUNCH("zk_attn_decode_qkv_sc");
     return 0;
 }
 

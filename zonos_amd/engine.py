@@ -153,8 +153,9 @@ class HipBackbone:
             kc, vt = self._kv(ws, i)
             call("zk_gemv_fused", ptr(x), D, ptr(L["wqkv"]), R, Nqkv, D, 0, ptr(L["ln1_w"]), ptr(L["ln1_b"]), c.eps,
                  ptr(part), None, skip, stream)
-            call("zk_attn_decode_qkv", ptr(part), 1, ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1,
-                 ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), self.rope_neox, skip, stream)
+            call("zk_attn_decode_qkv_sc", ptr(part), 1, ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"],
+                 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["attn_cnt"]), ptr(y),
+                 self.rope_neox, skip, stream)
             call("zk_gemv_fused", ptr(y), H * hd, ptr(L["wo"]), R, D, H * hd, 2, None, None, c.eps, None, ptr(x),
                  skip, stream)
             call("zk_gemv_fused", ptr(x), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, ptr(L["ln2_w"]), ptr(L["ln2_b"]),
@@ -187,9 +188,10 @@ class HipBackbone:
                 call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
             elif self.fuse_qkv:
                 # in_proj epilogue fused into the attention launch (position = ctx - 1 = scal[1])
-                call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
-                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), self.rope_neox,
-                     skip, stream)
+                # split partials (long contexts at small batch) merged inside the launch
+                call("zk_attn_decode_qkv_sc", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"],
+                     ptr(ws["attn_cnt"]) if "attn_cnt" in ws else None, ptr(y), self.rope_neox, skip, stream)
             else:
                 call("zk_qkv_rope", ptr(part), sp["qkv"], R, S, H, Hk, hd, ptr(self.freqs), 0, pos_dev, ptr(q),
                      ptr(kc), ptr(vt), ws["smax"], None, self.rope_neox, skip, stream)
@@ -249,6 +251,7 @@ class HipDecoder(HipBackbone):
         if self._ws is not None and self._ws["key"] == key:
             ws = self._ws
             ws["kv"].zero_()
+            ws["attn_cnt"].zero_()
             return ws
         self.release()
         D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
@@ -273,6 +276,7 @@ class HipDecoder(HipBackbone):
             q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
             h=torch.empty(Mp, Fd, dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
             attn_work=torch.empty(max(1, R * Hk * attn_splits * (8 + 4 * hd)), dtype=f32, device=dev),
+            attn_cnt=torch.zeros(R * Hk, dtype=i32, device=dev),     # in-launch split-combine tickets
             scal=torch.zeros(16, dtype=i32, device=dev),
             eos_mode=torch.zeros(B, dtype=i32, device=dev), steps_after=torch.zeros(B, dtype=i32, device=dev),
             remaining=torch.zeros(B, dtype=i32, device=dev), stopping=torch.zeros(B, dtype=i32, device=dev),
