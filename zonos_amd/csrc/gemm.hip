@@ -242,6 +242,7 @@ constexpr int WS_LDSPF = 1;      // chunks published ahead of the one being mult
 constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 
+
 // k_gemm_ws split-K slab stores (read once by the consumer kernel): non-temporal with ZK_SLAB_NT
 // (B=64: decode step 3.928 vs 3.959 ms; the B <= 8 GEMV keeps plain stores: its slabs are small
 // and nt cost 2.5 % per step at B=1)
