@@ -109,3 +109,45 @@ def test_hybrid_generate_teacher_forced_logits():
         worst = max(worst, float(e.max()))
         assert e.max() < 0.5 and e.mean() < 0.05, (s, e.max(), e.mean())
     print("hybrid teacher-forced logits: steps", n, "max abs err", worst)
+
+
+@pytest.mark.parametrize("hp,ds,nh,R,gs,pos", [(32, 64, 16, 6, 2, 5), (64, 128, 64, 8, 2, 6), (64, 128, 64, 3, 1, 7),
+                                               (64, 64, 16, 4, 4, 2)])
+def test_mamba_step_grouped_equals_per_head(hp, ds, nh, R, gs, pos, monkeypatch):
+    """The grouped decode kernel (heads per workgroup, B/C conv once per group, pipelined state
+    slices, whole-line state access at d_state 128) == the per-head kernel: SSM and conv states
+    bit for bit; the gated outputs bit for bit, or -- where the row sum y = C.h is reduced in a
+    different order (d_state 128: 16 lanes x 8 instead of 4 threads x 32) -- within 1 bf16 ulp of y."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator().manual_seed(hp + ds + R)
+    di = nh * hp
+    conv_dim = di + 2 * ds
+    ncol = 2 * di + 2 * ds + nh
+    parts = (torch.randn(gs, R, ncol, generator=g) * 0.5).to(DEV)
+    cw = (torch.randn(conv_dim, 4, generator=g) * 0.3).to(DEV)
+    cb = (torch.randn(conv_dim, generator=g) * 0.1).to(DEV)
+    conv0 = torch.randn(R, conv_dim, 4, generator=g).to(torch.bfloat16)
+    ssm0 = (0.5 * torch.randn(R, nh, hp, ds, generator=g)).to(torch.bfloat16)
+    A = (-torch.rand(nh, generator=g) * 4).to(DEV)
+    dtb = (torch.randn(nh, generator=g) * 0.5).to(DEV)
+    Dv = torch.randn(nh, generator=g).to(DEV)
+    posd = torch.tensor([pos], dtype=torch.int32, device=DEV)
+    s = stream_ptr()
+    outs = []
+    for grouped in ("0", "1"):
+        monkeypatch.setenv("ZK_MAMBA_GROUPED", grouped)
+        ca, cbuf = conv0.to(DEV), conv0.to(DEV)
+        ssm = ssm0.to(DEV)
+        yz = torch.full((R, di), float("nan"), device=DEV)
+        call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
+             ptr(ssm), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
+        torch.cuda.synchronize()
+        outs.append((ca.cpu(), cbuf.cpu(), ssm.cpu(), yz.cpu()))
+    for a, b, name in zip(outs[0][:3], outs[1][:3], ("conv_a", "conv_b", "ssm")):
+        assert torch.equal(a, b), name
+    ya, yb = outs[0][3], outs[1][3]
+    if ds != 128:
+        assert torch.equal(ya, yb)
+    else:
+        d = (ya - yb).abs()
+        assert float((d / ya.abs().clamp_min(1e-3)).max()) <= 2 ** -7 and float((d > 0).float().mean()) < 0.05

@@ -180,6 +180,38 @@ def attn_small():
                 print(f"attn R={R} ctx={ctx:5d} splits={ns:2d} {'in-launch combine' if sc else 'combine launch  ' if ns > 1 else 'unsplit         '}: {us:6.2f} us", flush=True)
 
 
+def mamba():
+    """Hybrid decode SSM update (zk_mamba_step) at c5 shapes: R=128 rows, 64 heads x 64 x 128 state,
+    in_proj split 2, rotating over 8 layers' states (1.1 GB: nothing stays in the MALL)."""
+    R, hp, ds, nh, gs = 128, 64, 128, 64, 2
+    di = nh * hp
+    conv_dim = di + 2 * ds
+    ncol = 2 * di + 2 * ds + nh
+    nl = 8
+    parts = torch.randn(gs, R, ncol, device=dev) * 0.5
+    cw = torch.randn(conv_dim, 4, device=dev) * 0.3
+    cb = torch.randn(conv_dim, device=dev) * 0.1
+    convs = [(torch.randn(R, conv_dim, 4, device=dev).to(torch.bfloat16),
+              torch.randn(R, conv_dim, 4, device=dev).to(torch.bfloat16)) for _ in range(nl)]
+    ssms = [(0.5 * torch.randn(R, nh, hp, ds, device=dev)).to(torch.bfloat16) for _ in range(nl)]
+    A = -torch.rand(nh, device=dev) * 4
+    dtb = torch.randn(nh, device=dev) * 0.5
+    Dv = torch.randn(nh, device=dev)
+    posd = torch.tensor([3], dtype=torch.int32, device=dev)
+    yz = torch.empty(R, di, device=dev)
+    it = [0]
+
+    def f():
+        i = it[0] % nl
+        it[0] += 1
+        call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(convs[i][0]), ptr(convs[i][1]),
+             ptr(posd), ptr(ssms[i]), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, S)
+    us = timeit(f, reps=40, warm=8)
+    b = R * di * ds * 2 * 2 + R * conv_dim * 8 * 2 + gs * R * ncol * 4 + R * di * 4
+    print(f"mamba_step R={R} grouped={os.environ.get('ZK_MAMBA_GROUPED', '1')}: {us:7.2f} us  "
+          f"{b / 1e6:6.1f} MB  {b / (us * 1e-6) / 1e9:6.0f} GB/s", flush=True)
+
+
 def attn_one(R, H, Hk, hd, ctx, smax, kcs, vts, q, ms_, ncopy):
     if True:
         work = torch.empty(R * Hk * ms_ * (8 + 4 * hd), device=dev)
@@ -266,6 +298,8 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
         gemm()
+    if what in ("mamba",):
+        mamba()
     if what in ("attn_small",):
         attn_small()
     if what in ("gemv",):

@@ -18,6 +18,7 @@
 #include "common.h"
 #include "../../include/zonos_hip.h"
 #include <algorithm>
+#include <stdlib.h>
 
 namespace {
 
@@ -26,6 +27,10 @@ constexpr int MB_MAXGS = 8;
 constexpr int GN_MAXJ = 16;      // k_gated_norm: row elements per thread held in registers (d_inner <= 4096)
 
 ZK_DEV float silu_f(float v) { return v / (1.0f + expf(-v)); }
+template <int R_>
+ZK_DEV float row_ror_f(float v) {      // DPP rotation inside each 16-lane row
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R_, 0xF, 0xF, false));
+}
 ZK_DEV float softplus_thr(float v) { return v <= 20.0f ? log1pf(expf(v)) : v; }
 
 // sum of the split-K slabs of one in_proj column, rounded to bf16 (the GEMM output dtype)
@@ -122,6 +127,196 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
         const float y = round_bf(acc + xp * Dv[h]);
         const float zz = s_z[p];
         yz[(size_t)r * di + h * HP + p] = y * (zz * (1.0f / (1.0f + expf(-zz))));
+    }
+}
+
+// Grouped form of k_mamba_step: one workgroup per (row, group of HG heads). The B / C conv
+// channels (2 * d_state of them, shared by all heads of a row) are computed once per group
+// instead of once per head, every prologue load is issued before the first one is waited for
+// (the in_proj slab columns, conv states and taps of all the group's channels), the first two
+// heads' SSM state slices are in flight during the prologue, and the heads are then streamed
+// with the next head's state loads in flight while the current one is updated. The per-element
+// arithmetic and the y reduction are those of k_mamba_step (bit-identical outputs and states).
+#ifndef ZK_MB_HG
+#define ZK_MB_HG 1                   // heads per workgroup (1: 54.4 us, 2: 60.2, 4: 61.9, 8: 68.6 at c5; tools/mamba_ab.sh)
+#endif
+#ifndef ZK_MB_PD
+#define ZK_MB_PD 1                   // heads' state slices in flight
+#endif
+template <int HP, int DS, int HG, int GS>
+__global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
+    const float* __restrict__ part, int R, int di, int nh, const float* __restrict__ conv_w,
+    const float* __restrict__ conv_b, const bf16_t* __restrict__ cs_a, bf16_t* __restrict__ cs_b,
+    const int32_t* __restrict__ pos_dev, bf16_t* __restrict__ ssm, const float* __restrict__ A,
+    const float* __restrict__ dt_bias, const float* __restrict__ Dv, float* __restrict__ yz,
+    const int32_t* __restrict__ skip) {
+    constexpr int TPP = MB_THREADS / HP;     // threads per headdim row
+    constexpr int EPT = DS / TPP;            // state elements per thread
+    constexpr int NV = EPT / 8;              // 16-B state loads per thread and head
+    constexpr int NX = HG * HP;              // x (and z) channels of the group
+    constexpr int NI = 2 * NX + 2 * DS + HG; // prologue items: x conv, B/C conv, z, dt
+    constexpr int NIT = (NI + MB_THREADS - 1) / MB_THREADS;
+    static_assert(TPP * HP == MB_THREADS && EPT * TPP == DS && EPT % 8 == 0, "tile");
+    __shared__ float s_x[NX], s_z[NX], s_B[DS], s_C[DS], s_dt[HG];
+    if (skip && *skip) return;
+    const int h0 = blockIdx.x * HG, r = blockIdx.y;
+    const int conv_dim = di + 2 * DS;
+    const int ncol = 2 * di + 2 * DS + nh;
+    const size_t slab = (size_t)R * ncol;
+    const float* prow = part + (size_t)r * ncol;
+    const int par = pos_dev ? (*pos_dev & 1) : 0;
+    const bf16_t* csi = (par ? cs_b : cs_a) + (size_t)r * conv_dim * 4;
+    bf16_t* cso = (par ? const_cast<bf16_t*>(cs_a) : cs_b) + (size_t)r * conv_dim * 4;
+    const int t = threadIdx.x, p = t / TPP, n0 = (t % TPP) * EPT;
+
+    // ---- prologue loads (all issued before any is used)
+    int col[NIT], ch[NIT];
+    float sv[NIT][GS];
+    uint2 cst[NIT];
+    float4 cw[NIT];
+    float cb[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+        const int i = min(t + MB_THREADS * k, NI - 1);
+        int c, cc;
+        if (i < NX) { cc = h0 * HP + i; c = di + cc; }                              // x conv channel
+        else if (i < NX + 2 * DS) { cc = di + (i - NX); c = di + cc; }              // B / C conv channel
+        else if (i < 2 * NX + 2 * DS) { cc = 0; c = h0 * HP + (i - NX - 2 * DS); }  // z column
+        else { cc = 0; c = 2 * di + 2 * DS + h0 + (i - 2 * NX - 2 * DS); }         // dt column
+        col[k] = c;
+        ch[k] = cc;
+#pragma unroll
+        for (int g = 0; g < GS; ++g) sv[k][g] = prow[(size_t)g * slab + c];
+        cst[k] = *reinterpret_cast<const uint2*>(csi + (size_t)cc * 4);
+        cw[k] = *reinterpret_cast<const float4*>(conv_w + (size_t)cc * 4);
+        cb[k] = conv_b[cc];
+    }
+    (void)col;
+    // the first PD heads' state slices. COAL (d_state = 128): every state load / store
+    // instruction of a wave covers 1 KB contiguous (8 whole 128-B lines) -- lane L of wave w holds,
+    // for v = 0..NV-1, row pv = (w*NV + v)*4 + L/16, channels 8*(L%16) .. +7 -- instead of 16 B of
+    // every 64 B (thread-contiguous 64-B runs: each instruction touching 32 lines partially).
+    constexpr bool COAL = DS == 128 && HP * DS / 8 == MB_THREADS * NV;
+    constexpr int PD = ZK_MB_PD < HG ? ZK_MB_PD : HG;
+    const int lw = t >> 6, ll = t & 63;
+    uint4 st[PD][NV];
+    auto st_off = [&](int v) -> size_t {        // element offset of piece v in the (row, head) state
+        if constexpr (COAL) return ((size_t)(lw * NV + v) * 64 + ll) * 8;
+        else return (size_t)p * DS + n0 + 8 * v;
+    };
+    auto load_state = [&](int hh, int buf) {
+        const bf16_t* sb = ssm + ((size_t)r * nh + h0 + hh) * HP * DS;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) st[buf][v] = *reinterpret_cast<const uint4*>(sb + st_off(v));
+    };
+#pragma unroll
+    for (int hh = 0; hh < PD; ++hh) load_state(hh, hh);
+
+    // ---- prologue arithmetic (the per-item arithmetic of k_mamba_step)
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+        const int i = t + MB_THREADS * k;
+        if (i >= NI) break;
+        float a = sv[k][0];
+#pragma unroll
+        for (int g = 1; g < GS; ++g) a += sv[k][g];
+        a = round_bf(a);                                                              // slab_col
+        if (i < NX + 2 * DS) {
+            const uint2 s2 = cst[k];
+            const float s1 = __uint_as_float((s2.x >> 16) << 16), sa = __uint_as_float((s2.y & 0xffffu) << 16);
+            const float s3 = __uint_as_float((s2.y >> 16) << 16);
+            float acc = cb[k];
+            acc += cw[k].x * s1;
+            acc += cw[k].y * sa;
+            acc += cw[k].z * s3;
+            acc += cw[k].w * a;
+            const float o = round_bf(silu_f(acc));
+            if (i < NX) s_x[i] = o;
+            else if (i < NX + DS) s_B[i - NX] = o;
+            else s_C[i - NX - DS] = o;
+            if (i < NX || h0 == 0) {
+                const uint32_t lo = (s2.x >> 16) | (s2.y << 16);
+                const uint32_t hi = (s2.y >> 16) | ((uint32_t)f2bf(a) << 16);
+                *reinterpret_cast<uint2*>(cso + (size_t)ch[k] * 4) = make_uint2(lo, hi);
+            }
+        } else if (i < 2 * NX + 2 * DS) {
+            s_z[i - NX - 2 * DS] = a;
+        } else {
+            s_dt[i - 2 * NX - 2 * DS] = a;
+        }
+    }
+    __syncthreads();
+
+    // ---- the group's heads, one state slice in flight ahead
+#pragma unroll
+    for (int hh = 0; hh < HG; ++hh) {
+        const int h = h0 + hh, buf = hh % PD;
+        const float dt = softplus_thr(s_dt[hh] + dt_bias[h]);
+        const float dA = expf(dt * A[h]);
+        if constexpr (COAL) {
+            bf16_t* sb = ssm + ((size_t)r * nh + h) * HP * DS;
+            const int nb = 8 * (ll & 15);
+            float Bv[8], Cv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { Bv[e] = s_B[nb + e] * dt; Cv[e] = s_C[nb + e]; }
+            float accv[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int pv = (lw * NV + v) * 4 + (ll >> 4);
+                const float xpv = s_x[hh * HP + pv];
+                float svv[8];
+                unpack8(st[buf][v], svv);
+                float a = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float sn = svv[e] * dA + Bv[e] * xpv;
+                    svv[e] = sn;
+                    a += sn * Cv[e];
+                }
+                accv[v] = a;
+                *reinterpret_cast<uint4*>(sb + st_off(v)) = pack8(svv);
+            }
+            if (hh + PD < HG) load_state(hh + PD, buf);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {         // sum over the row's 16 lanes (DPP rotations)
+                float a = accv[v];
+                a += row_ror_f<8>(a);
+                a += row_ror_f<4>(a);
+                a += row_ror_f<2>(a);
+                a += row_ror_f<1>(a);
+                const int pv = (lw * NV + v) * 4 + (ll >> 4);
+                if ((ll & 15) == 0) {
+                    const float y = round_bf(a + s_x[hh * HP + pv] * Dv[h]);
+                    const float zz = s_z[hh * HP + pv];
+                    yz[(size_t)r * di + h * HP + pv] = y * (zz * (1.0f / (1.0f + expf(-zz))));
+                }
+            }
+            continue;
+        }
+        const float xp = s_x[hh * HP + p];
+        bf16_t* sp = ssm + (((size_t)r * nh + h) * HP + p) * DS + n0;
+        float acc = 0.f;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            float svv[8];
+            unpack8(st[buf][v], svv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int n = n0 + 8 * v + e;
+                const float s = svv[e] * dA + (s_B[n] * dt) * xp;
+                svv[e] = s;
+                acc += s * s_C[n];
+            }
+            *reinterpret_cast<uint4*>(sp + 8 * v) = pack8(svv);
+        }
+        if (hh + PD < HG) load_state(hh + PD, buf);
+#pragma unroll
+        for (int off = 1; off < TPP; off <<= 1) acc += __shfl_xor(acc, off, 64);
+        if (t % TPP == 0) {
+            const float y = round_bf(acc + xp * Dv[h]);
+            const float zz = s_z[hh * HP + p];
+            yz[(size_t)r * di + h * HP + p] = y * (zz * (1.0f / (1.0f + expf(-zz))));
+        }
     }
 }
 
@@ -258,6 +453,35 @@ extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_in
     ZK_REQUIRE(gemm_nsplit >= 1 && gemm_nsplit <= MB_MAXGS, "zk_mamba_step: gemm_nsplit=%d", gemm_nsplit);
     ZK_REQUIRE(nheads * headdim == d_inner, "zk_mamba_step: nheads*headdim != d_inner");
     bool handled = false;
+    // grouped kernel: 8 heads per workgroup (B/C conv once per group), in_proj splits 1 / 2 / 4
+    const char* ge = getenv("ZK_MAMBA_GROUPED");   // "0": per-head kernel (A/B knob; read per launch call,
+    const bool grouped = !(ge && ge[0] == '0');    // graph replays do not call here)
+    if (grouped && nheads % ZK_MB_HG == 0 && (gemm_nsplit == 1 || gemm_nsplit == 2 || gemm_nsplit == 4)) {
+#define ZK_MB_STEPG(HP_, DS_)                                                                                       \
+    do {                                                                                                           \
+        const dim3 g_(nheads / ZK_MB_HG, R);                                                                              \
+        if (gemm_nsplit == 1)                                                                                      \
+            hipLaunchKernelGGL((k_mamba_step_g<HP_, DS_, ZK_MB_HG, 1>), g_, dim3(MB_THREADS), 0, (hipStream_t)stream,     \
+                               part, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,             \
+                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip);      \
+        else if (gemm_nsplit == 2)                                                                                 \
+            hipLaunchKernelGGL((k_mamba_step_g<HP_, DS_, ZK_MB_HG, 2>), g_, dim3(MB_THREADS), 0, (hipStream_t)stream,     \
+                               part, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,             \
+                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip);      \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_mamba_step_g<HP_, DS_, ZK_MB_HG, 4>), g_, dim3(MB_THREADS), 0, (hipStream_t)stream,     \
+                               part, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,             \
+                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip);      \
+    } while (0)
+        ZK_MB_DISPATCH(64, 128, ZK_MB_STEPG)
+        ZK_MB_DISPATCH(32, 64, ZK_MB_STEPG)
+        ZK_MB_DISPATCH(64, 64, ZK_MB_STEPG)
+#undef ZK_MB_STEPG
+        if (handled) {
+            ZK_CHECK_LAUNCH("zk_mamba_step");
+            return 0;
+        }
+    }
 #define ZK_MB_STEP(HP_, DS_)                                                                                       \
     hipLaunchKernelGGL((k_mamba_step<HP_, DS_>), dim3(nheads, R), dim3(MB_THREADS), 0, (hipStream_t)stream, part,  \
                        gemm_nsplit, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,                \
