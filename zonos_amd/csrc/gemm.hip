@@ -249,6 +249,9 @@ constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 #ifndef ZK_SLAB_NT
 #define ZK_SLAB_NT 1
 #endif
+#ifndef ZK_WS_EPI
+#define ZK_WS_EPI 1                // k_gemm_ws epilogue staged through LDS (whole-row stores)
+#endif
 ZK_DEV void st_slab(float* p, float v) {
     if constexpr (ZK_SLAB_NT) __builtin_nontemporal_store(v, p);
     else *p = v;
@@ -366,6 +369,64 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
             for (int mt = 0; mt < MT; ++mt)
                 acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(af[ch & 1][ks][mt]), b, acc[mt], 0, 0, 0);
         }
+    }
+    if (ZK_WS_EPI && (MODE == 1 || N % 4 == 0)) {
+        // Epilogue staged through the (now idle) LDS ring so that every store instruction writes
+        // whole rows: slabs 4 rows x 256 B (full 128-B lines) per instruction instead of 4 x 64-B
+        // pieces, SwiGLU 16 rows x 64 B instead of 16-B pieces. (The loader waves have exited; a
+        // workgroup barrier no longer counts them.)
+        constexpr int TS = 68;                                   // fp32 tile row stride (64 + pad)
+        float* tile = reinterpret_cast<float*>(smem);
+        __syncthreads();                                         // every wave's last LDS fragment read
+        if (MODE == 0) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) tile[(mt * 16 + lg * 4 + i) * TS + w * 16 + ln] = acc[mt][i];
+        } else {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float mine = round_bf(acc[mt][i]);
+                    const float other = __shfl_xor(mine, 8, 64);
+                    if (ln < 8) {
+                        const float sl = round_bf(other / (1.0f + expf(-other)));
+                        tile[(mt * 16 + lg * 4 + i) * TS + w * 8 + ln] = mine * sl;   // 32 output columns
+                    }
+                }
+        }
+        __syncthreads();
+        if (MODE == 0) {
+            float* C = Cpart + (size_t)split * M * N;
+            const int c4 = (lane & 15) * 4;
+#pragma unroll
+            for (int q = w; q < MT * 4; q += 4) {               // 4 rows x 256 B per instruction
+                const int m = q * 4 + (lane >> 4);
+                if (m < M && n0 + c4 < N) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(tile + m * TS + c4);
+                    float* dst = C + (size_t)m * N + n0 + c4;
+                    if (n0 + c4 + 3 < N) {
+                        if constexpr (ZK_SLAB_NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+                        else *reinterpret_cast<f32x4*>(dst) = v;
+                    } else {
+                        for (int e = 0; e < 4 && n0 + c4 + e < N; ++e) dst[e] = v[e];
+                    }
+                }
+            }
+        } else {
+            const int F = N / 2;
+            const int f0 = n0 / 2, c8 = (lane & 3) * 8;
+#pragma unroll
+            for (int q = w; q < MT; q += 4) {                    // 16 rows x 64 B per instruction
+                const int m = q * 16 + (lane >> 2);
+                if (m < M && f0 + c8 < F) {
+                    const float* src = tile + m * TS + c8;
+                    *reinterpret_cast<uint4*>(Cout + (size_t)m * F + f0 + c8) = pack8(src);
+                }
+            }
+        }
+        return;
     }
     if (MODE == 0) {
         float* C = Cpart + (size_t)split * M * N;
