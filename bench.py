@@ -174,6 +174,29 @@ def gemv_roofline(eng):
                  layers="rotating over all layers' fc1 weights")
 
 
+def step_small_roofline(eng, ctx):
+    """B <= 2 (c2): the persistent step kernel zk_decode_small (the whole backbone + norm_f + heads
+    of one decode step in one launch), launched back to back at the workload's mean context with
+    its own position word (the generate() state is left alone). Bytes per launch = every weight
+    once + the KV cache read at ctx + the new K/V rows (step_bytes)."""
+    import ctypes as C
+
+    import torch
+
+    from zonos_amd._lib import call
+    ws = eng._ws
+    R = ws["R"]
+    pos = torch.full((1,), ctx - 1, dtype=torch.int32, device=eng.device)
+    src = ws["small"]["args"]
+    args = type(src).from_buffer_copy(src)
+    args.pos_dev = pos.data_ptr()
+    args.skip = None
+    per = _time_launches([lambda st: call("zk_decode_small", C.byref(args), st)], reps=8)
+    eng._check_small(ws)
+    return _roof(step_bytes(eng, R, ctx), per, traffic=_pmc_traffic("k_decode_small", R=R, ctx=ctx),
+                 kernel="k_decode_small (zk_decode_small: persistent backbone + heads step)", M=R, ctx=ctx)
+
+
 def mamba_roofline(eng):
     """Hybrid (c5): zk_mamba_step (the SSM state update, HBM-bound) over every Mamba layer's state
     in turn; algorithmic bytes = SSM state read + write (R*d_inner*d_state*2 B each) + conv state
@@ -354,6 +377,8 @@ class GpuWorkload:
         ctx_mean = args.lc + args.prefix + 1 + n_dec // 2
         if args.model == "hybrid":
             roof = mamba_roofline(eng)
+        elif "small" in eng._ws:
+            roof = step_small_roofline(eng, ctx_mean)
         elif eng._small(R):
             roof = gemv_roofline(eng)
         else:

@@ -12,35 +12,14 @@
 //
 // KV cache layout: see "KV cache layout" below (32-key slices in MFMA-fragment order).
 #include "common.h"
+#include "attn_common.h"
 #include "../../include/zonos_hip.h"
 #include <algorithm>
 #include <stdlib.h>
 
 namespace {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-ZK_DEV bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
-
-// ------------------------------------------------------------------ KV cache layout
-// Per (row, kv head) the cache holds Smax keys in 32-key slices of 8 KB. Inside a slice the
-// data is stored in exactly the order the decode wave's MFMA fragments consume it, so every
-// fragment load is one contiguous 1 KB read:
-//   K: [slice][h 2][ks 4][lane 64][8]  lane = 16*lg + ln holds key 8*(ln>>2) + 4h + (ln&3)
-//      of the slice, dims 32ks + 8lg .. +8          (A operand of S^T = K.Q^T)
-//   V: [slice][dt 8][lane 64][8]       lane holds channel 16dt + ln, keys 8lg .. 8lg+7
-//                                                  (A operand of O^T = V^T.P^T)
-// Element offsets within one (row, kv head) block of Smax*128 elements:
-ZK_DEV size_t k_off(int key, int c8) {      // dims 8*c8 .. 8*c8+7 of key
-    const int o = key & 31, grp = o >> 3, h = (o >> 2) & 1, i = o & 3;
-    const int ln = 4 * grp + i, ks = c8 >> 2, lg = c8 & 3;
-    return (size_t)(key >> 5) * 4096 + ((h * 4 + ks) * 64 + lg * 16 + ln) * 8;
-}
-ZK_DEV size_t v_off(int key, int ch) {      // channel ch of key
-    const int o = key & 31, lg = o >> 3, e = o & 7;
-    return (size_t)(key >> 5) * 4096 + ((ch >> 4) * 64 + lg * 16 + (ch & 15)) * 8 + e;
-}
 
 // ------------------------------------------------------------------ LayerNorm helper
 // Row of D elements, 8 per thread (D = 8 * NT * n8). Two-pass mean/var in fp32,
@@ -314,15 +293,6 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln_d2k(const float* part, int n
     *reinterpret_cast<uint2*>(xn_out + (size_t)row * D + c1) = make_uint2(pack2(o[4], o[5]), pack2(o[6], o[7]));
 }
 
-// ------------------------------------------------------------------ in_proj epilogue
-// RoPE pair j (0..hd/2-1) of a head: interleaved (_torch.py:18-30: dims 2j, 2j+1) or, NEOX,
-// GPT-NeoX "rotate half" (flash_attn apply_rotary, interleaved=False: dims j, j + hd/2).
-// Both use (cos, sin) entry j of the position's [hd/2][2] table.
-template <bool NEOX>
-ZK_DEV void rope_dims(int j, int hd, int& d0, int& d1) {
-    d0 = NEOX ? j : 2 * j;
-    d1 = NEOX ? j + hd / 2 : 2 * j + 1;
-}
 
 template <bool NEOX>
 __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv,
@@ -374,340 +344,6 @@ __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit,
     }
 }
 
-// ------------------------------------------------------------------ decode attention
-constexpr int AT_KB = 128;      // keys per workgroup iteration (4 waves x 32)
-constexpr int AT_G = 4;         // query heads per KV head handled by the B operand (<= 16)
-constexpr int AT_STR = 2 * AT_G + AT_G * 128;   // work floats per (r, g, split)
-constexpr int AT_MAXGS = 8;     // max in_proj split-K slabs the fused prologue reduces
-
-// One 32-key step of one wave: registers for K (A operand of S^T = K.Q^T) and V^T
-// (A operand of O^T = V^T.P^T). Key mapping inside the 32: MFMA row r = 4*grp + i of tile h
-// holds key 8*grp + 4*h + i, so a lane's 8 score values are the 8 CONTIGUOUS keys
-// 8*grp .. 8*grp+7 and its V^T fragment is one 16-byte load.
-struct KVFrag {
-    uint4 k[2][4];   // [tile h][d-step]
-    uint4 v[8];      // [d-tile]
-};
-
-// KV cache slices. NT: loaded non-temporally -- chosen by the host when one launch streams
-// >= KV_NT_BYTES of cache (B=64: 0.8 GB, read once per step, far beyond L2 and the MALL: nt 3.815
-// vs 3.954 ms per decode step); small caches (B=1: 4 MB per layer) stay MALL-resident across
-// steps and plain loads keep them there (1.32 vs 1.35 ms per step).
-constexpr double KV_NT_BYTES = 64e6;
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
-template <bool NT>
-ZK_DEV uint4 ld_kv(const bf16_t* p) {
-    if constexpr (NT) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p)));
-    else return *reinterpret_cast<const uint4*>(p);
-}
-
-template <bool NT>
-ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int key_base, int ln, int lg) {
-    (void)Smax;
-    const int lane = lg * 16 + ln;
-    const bf16_t* k0 = kb + (size_t)(key_base >> 5) * 4096 + lane * 8;
-    const bf16_t* v0 = vb + (size_t)(key_base >> 5) * 4096 + lane * 8;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = ld_kv<NT>(k0 + (h * 4 + ks) * 512);
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld_kv<NT>(v0 + dt * 512);
-}
-
-struct AttnState {
-    float m, l;
-    f32x4 o[8];      // o[dt][i] = O^T[d = dt*16 + 4lg + i][head = ln]
-};
-
-ZK_DEV void attn_step(AttnState& st, const KVFrag& f, const bf16x8* qf, int key_base, int ctx, float scale,
-                      int lg) {
-    f32x4 sacc[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        sacc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            sacc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(f.k[h][ks]), qf[ks], sacc[h], 0, 0, 0);
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int key = key_base + 8 * lg + 4 * h + i;
-            const float sv = key < ctx ? sacc[h][i] * scale : -INFINITY;
-            sacc[h][i] = sv;
-            mx = fmaxf(mx, sv);
-        }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(st.m, mx);
-    if (mn == -INFINITY) return;                       // nothing visible yet (all keys masked)
-    const float corr = (st.m == -INFINITY) ? 0.f : __expf(st.m - mn);
-    float ps = 0.f;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float pv = __expf(sacc[h][i] - mn);
-            sacc[h][i] = pv;
-            ps += pv;
-        }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
-    st.l = st.l * corr + ps;
-    st.m = mn;
-    const uint4 pa = make_uint4(pack2(sacc[0][0], sacc[0][1]), pack2(sacc[0][2], sacc[0][3]),
-                                pack2(sacc[1][0], sacc[1][1]), pack2(sacc[1][2], sacc[1][3]));
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st.o[dt][i] *= corr;
-        st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(f.v[dt]), as_frag(pa), st.o[dt], 0, 0, 0);
-    }
-}
-
-// Flash-decoding over the KV cache: grid (nsplit, Hkv, R); each workgroup streams its share
-// of 128-key blocks, each wave a 32-key slice of every block, with the next slice's K/V
-// loads in flight (two register sets) while the current one is multiplied; the 4 waves merge
-// (m, l, O) through LDS at the end. nsplit == 1 writes the normalised bf16 output directly.
-// Replace the newest key's K row / V^T entries in a loaded 32-key slice by the values kept in
-// LDS (their cache lines are written at the end of the fused kernel). Wave-uniform early out.
-ZK_DEV void patch_kv(KVFrag& f, const uint32_t* s_kn, const uint16_t* s_vn, int key_base, int pos, int ln, int lg) {
-    if (pos < key_base || pos >= key_base + 32) return;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int key = key_base + 8 * (ln >> 2) + 4 * h + (ln & 3);
-        if (key == pos) {
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) f.k[h][ks] = *reinterpret_cast<const uint4*>(s_kn + ks * 16 + lg * 4);
-        }
-    }
-    const int e = pos - key_base - 8 * lg;      // element of this lane's 8-key V^T group
-    if (e >= 0 && e < 8) {
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-            uint16_t tmp[8];
-            *reinterpret_cast<uint4*>(tmp) = f.v[dt];
-            tmp[e] = s_vn[dt * 16 + ln];
-            f.v[dt] = *reinterpret_cast<const uint4*>(tmp);
-        }
-    }
-}
-
-// FUSED: the in_proj epilogue (k_qkv_rope) runs as this kernel's prologue -- each workgroup
-// reduces the split-K slabs of its own 4 query heads + 1 KV head (768 columns), applies RoPE,
-// keeps q in LDS and (the split that owns the newest key) stores the new K / V^T entries
-// before the key loop reads them. One launch per layer instead of two.
-// COMB (nsplit > 1): the splits of one (row, kv head) combine in this launch instead of in
-// k_attn_combine -- each workgroup publishes its partial (m, l, O) (stores drained, agent-scope
-// release) and takes a ticket on cnt[row][kv head]; the workgroup drawing the last ticket of the
-// launch (tickets are monotonic: the count is a multiple of nsplit before every launch) acquires
-// and merges all nsplit partials exactly as k_attn_combine does. Saves the combine launch.
-template <bool FUSED, bool NEOX, bool KVNT, bool COMB = false>
-__global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H,
-                                                        int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
-                                                        float* work, float scale, bf16_t* out, const int32_t* skip,
-                                                        const float* part, int gsplit, const float* freqs,
-                                                        uint32_t* cnt = nullptr) {
-    constexpr int HD = 128;
-    __shared__ float s_m[4][16];
-    __shared__ float s_l[4][16];
-    __shared__ float s_o[4][AT_G][HD];
-    __shared__ __attribute__((aligned(16))) uint32_t s_q[AT_G][HD / 2];
-    __shared__ __attribute__((aligned(16))) uint32_t s_kn[HD / 2];   // new key (post-RoPE), bf16 pairs
-    __shared__ uint16_t s_vn[HD];                                    // new value
-    __shared__ int s_last;                                           // COMB: this workgroup merges
-    if (skip && *skip) return;
-    const int split = blockIdx.x, nsplit = gridDim.x, g = blockIdx.y, r = blockIdx.z;
-    const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
-    const int nkb = (ctx + AT_KB - 1) / AT_KB;
-    const int kb0 = (int)((long)split * nkb / nsplit), kb1 = (int)((long)(split + 1) * nkb / nsplit);
-    const int G = H / Hkv;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int ln = lane & 15, lg = lane >> 4;
-    bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
-    bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
-
-    bf16x8 qf[4];
-    KVFrag fa, fb;
-    const int last = kb1 - 1;
-    // the first key block can be fetched before the prologue unless it holds the new key
-    // FUSED: the new key's cache lines are written only at the end of the kernel (a store
-    // followed by loads of the same partially written lines stalls the key loop); the key loop
-    // patches the new K/V into its registers from LDS instead, so the arithmetic is exactly
-    // that of reading the cache. The first key block can therefore be fetched before the prologue.
-    const int pos = ctx - 1;
-    const bool early = FUSED && kb1 > kb0;
-    if (early) {      // the first TWO key blocks are in flight during the prologue
-        load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
-        load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
-    }
-    if constexpr (FUSED) {
-        // pairs: [0, G*64) q of heads g*G.., then 64 k pairs, then 64 v pairs
-        const int N = (H + 2 * Hkv) * HD;
-        const size_t slab = (size_t)R * N;
-        const float* prow = part + (size_t)r * N;
-        const float* fc = freqs + (size_t)pos * HD;
-        uint16_t* q16 = reinterpret_cast<uint16_t*>(&s_q[0][0]);
-        uint16_t* k16 = reinterpret_cast<uint16_t*>(s_kn);
-        for (int pi = threadIdx.x; pi < (G + 2) * (HD / 2); pi += 256) {
-            const int hp = pi / (HD / 2), j = pi % (HD / 2);      // hp < G: q head g*G+hp; G: k; G+1: v
-            int d0, d1;
-            rope_dims<NEOX>(j, HD, d0, d1);
-            const int cb = hp < G ? (g * G + hp) * HD : (hp == G ? H * HD + g * HD : (H + Hkv) * HD + g * HD);
-            // all slab loads issued together (clamped slab index, select after) -- same
-            // left-to-right fp32 sum as k_qkv_rope
-            float v0[AT_MAXGS], v1[AT_MAXGS];
-#pragma unroll
-            for (int sl = 0; sl < AT_MAXGS; ++sl) {
-                const float* ps = prow + (size_t)min(sl, gsplit - 1) * slab + cb;
-                v0[sl] = ps[d0];
-                v1[sl] = ps[d1];
-            }
-            const float2 cs = *reinterpret_cast<const float2*>(fc + 2 * j);
-            float a = v0[0], bb = v1[0];
-#pragma unroll
-            for (int sl = 1; sl < AT_MAXGS; ++sl)
-                if (sl < gsplit) { a += v0[sl]; bb += v1[sl]; }
-            a = round_bf(a);
-            bb = round_bf(bb);
-            if (hp <= G) {
-                const float o0 = __fsub_rn(__fmul_rn(a, cs.x), __fmul_rn(bb, cs.y));
-                const float o1 = __fadd_rn(__fmul_rn(bb, cs.x), __fmul_rn(a, cs.y));
-                uint16_t* dst = hp < G ? q16 + hp * HD : k16;
-                dst[d0] = f2bf(o0);
-                dst[d1] = f2bf(o1);
-            } else {
-                s_vn[d0] = f2bf(a);
-                s_vn[d1] = f2bf(bb);
-            }
-        }
-        __syncthreads();      // q, new k, new v in LDS
-#ifdef ZK_ATT_DBGQ
-        if (q != nullptr && split == 0)
-            for (int i = threadIdx.x; i < G * HD / 2; i += 256)
-                reinterpret_cast<uint32_t*>(const_cast<bf16_t*>(q))[((size_t)r * H + g * G) * (HD / 2) + i] =
-                    s_q[i / (HD / 2)][i % (HD / 2)];
-#endif
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (ln < G) v = *reinterpret_cast<const uint4*>(&s_q[ln][ks * 16 + lg * 4]);
-            qf[ks] = as_frag(v);
-        }
-    } else {
-        const bf16_t* qr = q + (size_t)r * H * HD + (size_t)(g * G + ln) * HD;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (ln < G) v = *reinterpret_cast<const uint4*>(qr + ks * 32 + lg * 8);
-            qf[ks] = as_frag(v);
-        }
-    }
-    AttnState st;
-    st.m = -INFINITY;
-    st.l = 0.f;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    if (kb1 > kb0) {
-        if (!early) load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
-        for (int it = kb0; it < kb1; it += 2) {
-            if (!(early && it == kb0)) load_kv<KVNT>(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
-            if (FUSED) patch_kv(fa, s_kn, s_vn, it * AT_KB + 32 * w, pos, ln, lg);
-            attn_step(st, fa, qf, it * AT_KB + 32 * w, ctx, scale, lg);
-            load_kv<KVNT>(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
-            if (it + 1 < kb1) {
-                if (FUSED) patch_kv(fb, s_kn, s_vn, (it + 1) * AT_KB + 32 * w, pos, ln, lg);
-                attn_step(st, fb, qf, (it + 1) * AT_KB + 32 * w, ctx, scale, lg);
-            }
-        }
-    }
-    if (FUSED && split == nsplit - 1) {      // the split owning the newest key stores it (cache for later steps)
-        const int t = threadIdx.x;
-        if (t < HD / 2) *reinterpret_cast<uint32_t*>(kb + k_off(pos, t >> 2) + ((2 * t) & 7)) = s_kn[t];
-        else if (t < HD / 2 + HD) reinterpret_cast<uint16_t*>(vb)[v_off(pos, t - HD / 2)] = s_vn[t - HD / 2];
-    }
-    // merge the 4 waves
-    if (lg == 0) { s_m[w][ln] = st.m; s_l[w][ln] = st.l; }
-    __syncthreads();
-    const float M = fmaxf(fmaxf(s_m[0][ln], s_m[1][ln]), fmaxf(s_m[2][ln], s_m[3][ln]));
-    const float cw = (st.m == -INFINITY) ? 0.f : __expf(st.m - M);
-    if (ln < AT_G) {
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s_o[w][ln][dt * 16 + lg * 4 + i] = st.o[dt][i] * cw;
-    }
-    __syncthreads();
-    if (nsplit == 1) {
-        // normalised output for the G heads: thread -> (head, 2 channels)
-        for (int i = threadIdx.x; i < G * HD / 2; i += 256) {
-            const int h = i / (HD / 2), d = (i % (HD / 2)) * 2;
-            float Mh = -INFINITY;
-            for (int k = 0; k < 4; ++k) Mh = fmaxf(Mh, s_m[k][h]);
-            float L = 0.f;
-            for (int k = 0; k < 4; ++k) L += (s_m[k][h] == -INFINITY) ? 0.f : s_l[k][h] * __expf(s_m[k][h] - Mh);
-            const float o0 = s_o[0][h][d] + s_o[1][h][d] + s_o[2][h][d] + s_o[3][h][d];
-            const float o1 = s_o[0][h][d + 1] + s_o[1][h][d + 1] + s_o[2][h][d + 1] + s_o[3][h][d + 1];
-            const float inv = 1.0f / L;
-            *reinterpret_cast<uint32_t*>(out + (size_t)r * H * HD + (size_t)(g * G + h) * HD + d) =
-                pack2(o0 * inv, o1 * inv);
-        }
-        return;
-    }
-    float* wp = work + (((size_t)r * Hkv + g) * nsplit + split) * AT_STR;
-    for (int i = threadIdx.x; i < AT_G * HD; i += 256) {
-        const int h = i / HD, d = i % HD;
-        wp[2 * AT_G + i] = s_o[0][h][d] + s_o[1][h][d] + s_o[2][h][d] + s_o[3][h][d];
-    }
-    if (threadIdx.x < AT_G) {
-        const int h = threadIdx.x;
-        float Mh = -INFINITY;
-        for (int k = 0; k < 4; ++k) Mh = fmaxf(Mh, s_m[k][h]);
-        float L = 0.f;
-        for (int k = 0; k < 4; ++k) L += (s_m[k][h] == -INFINITY) ? 0.f : s_l[k][h] * __expf(s_m[k][h] - Mh);
-        wp[h] = Mh;
-        wp[AT_G + h] = L;
-    }
-    if constexpr (COMB) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // keep the fence's wait (ROCm 7.2)
-            const uint32_t old = __hip_atomic_fetch_add(cnt + (size_t)r * Hkv + g, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            s_last = ((old + 1) % (uint32_t)nsplit) == 0;
-        }
-        __syncthreads();
-        if (!s_last) return;
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        const float* base = work + ((size_t)r * Hkv + g) * nsplit * AT_STR;
-        for (int i = threadIdx.x; i < G * HD / 2; i += 256) {       // k_attn_combine's arithmetic
-            const int j = i / (HD / 2), d = (i % (HD / 2)) * 2;
-            float M = -INFINITY;
-            for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, base[sp * AT_STR + j]);
-            float L = 0.f, o0 = 0.f, o1 = 0.f;
-            for (int sp = 0; sp < nsplit; ++sp) {
-                const float* p = base + sp * AT_STR;
-                const float c = (p[j] == -INFINITY) ? 0.f : __expf(p[j] - M);
-                L += p[AT_G + j] * c;
-                o0 += p[2 * AT_G + j * HD + d] * c;
-                o1 += p[2 * AT_G + j * HD + d + 1] * c;
-            }
-            const float inv = 1.0f / L;
-            *reinterpret_cast<uint32_t*>(out + (size_t)r * H * HD + (size_t)(g * G + j) * HD + d) =
-                pack2(o0 * inv, o1 * inv);
-        }
-    }
-}
 
 __global__ __launch_bounds__(64) void k_attn_combine(const float* work, int H, int Hkv, int nsplit, bf16_t* out,
                                                      const int32_t* skip) {

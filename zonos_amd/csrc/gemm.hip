@@ -567,34 +567,6 @@ ZK_DEV void opaque(uint4& v) {
     v = __builtin_bit_cast(uint4, t);
 }
 
-// DPP row rotation (within each 16-lane row) of a 32-bit value
-template <int R>
-ZK_DEV float row_ror(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xF, 0xF, false));
-}
-template <int R>
-ZK_DEV uint4 row_ror4(uint4 v) {
-    uint4 o;
-    o.x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x120 + R, 0xF, 0xF, false);
-    o.y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x120 + R, 0xF, 0xF, false);
-    o.z = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x120 + R, 0xF, 0xF, false);
-    o.w = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x120 + R, 0xF, 0xF, false);
-    return o;
-}
-// wave64 sum without LDS permutes: rotations inside each 16-lane row, then the 4 row sums
-// (read lanes 0, 16, 32, 48) added in row order. Every lane gets the same value.
-ZK_DEV float wave_sum_dpp(float v) {
-    v += row_ror<8>(v);
-    v += row_ror<4>(v);
-    v += row_ror<2>(v);
-    v += row_ror<1>(v);
-    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-    return ((r0 + r1) + r2) + r3;
-}
-
 constexpr int GF_XS = 2048 + 8;    // LDS row stride (bf16) of the LayerNorm'd rows (K = 2048)
 
 // NW waves split K (wave w: K range w/NW); KS k-steps of 32 per wave; PF loads in flight.

@@ -216,6 +216,11 @@ class HipDecoder(HipBackbone):
     # B <= 8 decode (R <= 16 rows) runs each block as five launches (zk_gemv_fused: LayerNorm
     # prologues, residual epilogues, no split-K slabs) instead of seven; ZK_SMALL=0 disables it
     small_batch_path = os.environ.get("ZK_SMALL", "1") != "0"
+    # B <= 2 (R <= 4 rows) at the Zonos-v0.1-transformer geometry: the whole step's backbone +
+    # heads as ONE persistent launch (zk_decode_small, csrc/step_small.hip), bit-identical to the
+    # five-launch-per-block sequence (with ZK_GF_LAYOUT=1). Opt-in (ZK_PERSIST=1): measured 2.4x
+    # SLOWER than the launches (2.85 vs 1.20 ms per c2 step; DESIGN.md §6, profiles/r2_s3_step_small_*)
+    persistent_small = os.environ.get("ZK_PERSIST", "0") == "1"
 
     def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
         super().__init__(cfg, weights, device)
@@ -252,6 +257,8 @@ class HipDecoder(HipBackbone):
             ws = self._ws
             ws["kv"].zero_()
             ws["attn_cnt"].zero_()
+            if "small" in ws:
+                ws["small"]["sync"].zero_()
             return ws
         self.release()
         D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
@@ -286,8 +293,54 @@ class HipDecoder(HipBackbone):
             dbg=torch.empty(B, N_CB, VOCAB, dtype=f32, device=dev),
             graph=None,
         )
+        if self._persist(R):
+            ws["small"] = self._small_ws(ws, R)
         self._ws = ws
         return ws
+
+    def _persist(self, R: int) -> bool:
+        c = self.cfg
+        return (self.persistent_small and R <= 4 and c.d_model == 2048 and c.n_heads == 16 and c.n_kv == 4
+                and c.head_dim == 128 and c.d_ff == 8192 and self.rope_neox == 0)
+
+    def _small_ws(self, ws, R: int) -> dict:
+        """Buffers + device layer table of the persistent small-batch step (zk_decode_small)."""
+        c = self.cfg
+        dev = self.device
+        f32, bf = torch.float32, torch.bfloat16
+        D, Fd, Nqkv = c.d_model, c.d_ff, (c.n_heads + 2 * c.n_kv) * c.head_dim
+        nh = N_CB * VOCAB
+        # attention key splits (merged inside the launch): enough units to spread the KV stream of
+        # the R x 4 (row, kv head) pairs over ~64 CUs; ZK_ATTN_SPLITS pins it (same knob as the launch path)
+        env = os.environ.get("ZK_ATTN_SPLITS")
+        nsp = max(1, min(ws["smax"] // 128, int(env) if env else 64 // (R * c.n_kv)))
+        table = []
+        for i, L in enumerate(self.layers):
+            kc, vt = self._kv(ws, i)
+            table.append([ptr(L["wqkv"]), ptr(L["wo"]), ptr(L["fc1"]), ptr(L["fc2"]), ptr(L["ln1_w"]), ptr(L["ln1_b"]),
+                          ptr(L["ln2_w"]), ptr(L["ln2_b"]), ptr(kc), ptr(vt)])
+        sw = dict(
+            layers=torch.tensor(table, dtype=torch.int64, device=dev),
+            xm=torch.empty(R, D, dtype=bf, device=dev), p_qkv=torch.empty(4, R, Nqkv, dtype=f32, device=dev),
+            p_o=torch.empty(4, R, D, dtype=f32, device=dev), p_f=torch.empty(4, R, D, dtype=f32, device=dev),
+            p_heads=torch.empty(4, R, nh, dtype=f32, device=dev),
+            sync=torch.zeros(_lib.load().zk_small_sync_words(c.n_layer), dtype=torch.int32, device=dev),
+            attn_work=torch.empty(R * c.n_kv * nsp * (8 + 4 * c.head_dim), dtype=f32, device=dev),
+        )
+        scal = ws["scal"]
+        sw["args"] = _lib.SmallArgs(
+            ptr(sw["layers"]), c.n_layer, R, ws["smax"], nh, ptr(self.heads), ptr(self.lnf_w), ptr(self.lnf_b),
+            c.eps, ptr(self.freqs), ptr(scal[1:2]), ptr(ws["x"]), ptr(sw["xm"]), ptr(sw["p_qkv"]), ptr(ws["y"]),
+            ptr(sw["p_o"]), ptr(ws["h"]), ptr(sw["p_f"]), ptr(sw["p_heads"]), ptr(sw["sync"]), ptr(scal[3:4]),
+            nsp, ptr(sw["attn_work"]), None)
+        return sw
+
+    def _check_small(self, ws):
+        """A dependency wait inside zk_decode_small that gave up leaves a code in sync[32]."""
+        if "small" in ws:
+            err = int(ws["small"]["sync"][32].item())
+            if err:
+                raise _lib.ZonosHipError(f"zk_decode_small: dependency wait gave up (code {err:#x})")
 
     def release(self):
         if self._ws is not None and self._ws.get("graph"):
@@ -318,11 +371,16 @@ class HipDecoder(HipBackbone):
         scal = ws["scal"]
         skip = ptr(scal[3:4])
         L0 = self.layers[0]
-        small = self._small(R)      # small path: layer 0's LayerNorm runs in the in_proj prologue
+        small = self._small(R) or "small" in ws      # layer 0's LayerNorm runs in the in_proj prologue
         call("zk_embed_codes", ptr(ws["delayed"]), B, 1, N_CB, ws["Ld"] * N_CB, ws["Ld"], ptr(scal[0:1]), -1,
              ptr(self.emb), VOCAB, c.d_model, 2, ptr(ws["x"]), 1, 0, None if small else ptr(L0["ln1_w"]),
              None if small else ptr(L0["ln1_b"]), c.eps, None if small else ptr(ws["xn"]), skip, stream)
-        if self._small(R):
+        logits, nsp = ws["part"], ws["splits"]["heads"]
+        if "small" in ws:
+            # backbone + norm_f + heads in one persistent launch; heads as 4 K-quarter slabs
+            call("zk_decode_small", C_ref(ws["small"]["args"]), stream)
+            logits, nsp = ws["small"]["p_heads"], 4
+        elif self._small(R):
             self._layers_small(ws, R, stream, skip)
             # heads with the final LayerNorm (norm_f) as the GEMV prologue: one fp32 slab
             call("zk_gemv_fused", ptr(ws["x"]), c.d_model, ptr(self.heads), R, N_CB * VOCAB, c.d_model, 0,
@@ -330,9 +388,8 @@ class HipDecoder(HipBackbone):
         else:
             self._layers(ws, R, R, 1, False, stream, skip)
             self._heads(ws, R, 1, stream, skip)
-        nsp = ws["splits"]["heads"]
-        call("zk_sample_heads", ptr(ws["part"]), nsp, C_ref(st), C_ref(sp), 0, 0, ptr(ws["dbg"]), stream)
-        call("zk_sample_heads", ptr(ws["part"]), nsp, C_ref(st), C_ref(sp), 0, 1, None, stream)
+        call("zk_sample_heads", ptr(logits), nsp, C_ref(st), C_ref(sp), 0, 0, ptr(ws["dbg"]), stream)
+        call("zk_sample_heads", ptr(logits), nsp, C_ref(st), C_ref(sp), 0, 1, None, stream)
         call("zk_eos_step", C_ref(st), 0, 0, stream)
 
     def _small(self, R: int) -> bool:
@@ -437,6 +494,7 @@ class HipDecoder(HipBackbone):
                 trace["tokens"].append(ws["delayed"][..., off:off + 1].clone())
             if int(scal[3]):
                 break
+        self._check_small(ws)
         offset = int(ws["scal"][0].item()) - 1
         if trace is not None:
             trace["delayed"] = ws["delayed"].clone()
