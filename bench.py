@@ -361,7 +361,7 @@ class GpuWorkload:
         t2 = time.time()
         if self.dist is not None:
             from zonos_amd.distributed import gather_codes
-            gather_codes(codes, device=self.dev)
+            gather_codes(codes, device=self.coll_dev)
         if timed:
             self.stats["gen_s"] += t1 - t0
             self.stats["dac_s"] += t2 - t1
@@ -414,12 +414,19 @@ def main():
             dist.init_process_group("gloo")
         wl = StubWorkload(args, rank, world, dist)
     else:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        # ZK_BENCH_SHARE_GPU=1: rehearsal of the N-rank path on a one-GPU box -- every rank on
+        # cuda:0 and the collectives over gloo on host tensors (RCCL refuses two ranks on one GPU)
+        share = os.environ.get("ZK_BENCH_SHARE_GPU") == "1"
+        torch.cuda.set_device(0 if share else local)
+        dev = torch.device("cuda", 0 if share else local)
         if world > 1:
             import torch.distributed as dist
-            dist.init_process_group("nccl", device_id=dev)
+            if share:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=dev)
         wl = GpuWorkload(args, rank, world, dist, dev)
+        wl.coll_dev = torch.device("cpu") if share else dev
 
     for i in range(args.warmup):
         wl.step(i, False)
@@ -435,7 +442,7 @@ def main():
         dist.barrier()
     elapsed = time.time() - t0
     if dist is not None:
-        dev_ = "cpu" if args.stub else torch.device("cuda", local)
+        dev_ = "cpu" if args.stub else wl.coll_dev
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev_)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
