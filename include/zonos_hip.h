@@ -157,6 +157,10 @@ typedef struct zk_small_args {
                                        100 MHz) [ncu][n_layer * 5 + 2][4] -- profiling only */
 } zk_small_args;
 int zk_small_sync_words(int n_layer);
+/* Cache warming (tuning experiments): read nseg segments of seg_bytes at stride seg_stride with
+ * the given policy (0 plain, 1 non-temporal) and discard them, leaving them in the Infinity Cache. */
+int zk_prefetch(const void* base, long seg_stride, long seg_bytes, int nseg, int mode, int nblocks,
+                uint32_t* sink, void* stream);
 int zk_decode_small(const zk_small_args* a, void* stream);
 /* fc1 weight [2F][D] (rows: F "y" then F "gate") -> interleaved groups of 8 y + 8 gate rows. */
 int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream);

@@ -60,6 +60,7 @@ _SIGS = {
     "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
     "zk_gemv_fused": [P, L, P, I, I, I, I, P, P, F, P, P, P, P],
     "zk_decode_small": [C.POINTER(SmallArgs), P],
+    "zk_prefetch": [P, L, L, I, I, I, P, P],
     "zk_permute_fc1": [P, I, I, P, P],
     "zk_pack_weights": [P, I, I, P, P],
     "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, I, P, P],

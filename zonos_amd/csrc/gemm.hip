@@ -666,8 +666,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict_
         // y = (x - mean) * rstd * w + b rounded to bf16 -- the arithmetic of ln_row_pre)
         bf16_t* xsb = reinterpret_cast<bf16_t*>(xs);
 #pragma unroll
-        for (int rr = 0; rr < MR; ++rr) {       // unconditional (clamped rows): the loads above
-            const int m = w + NW * rr;            // stay where they are, only the store is masked
+        for (int rr = 0; rr < MR; ++rr) {       // the (clamped) loads above were issued for every
+            const int m = w + NW * rr;            // row; only rows < M are normalised (wave-uniform)
+            if (m >= M) break;
             float xf[NJ * 8];
 #pragma unroll
             for (int j = 0; j < NJ; ++j) unpack8(xv[rr][j], xf + 8 * j);
@@ -689,7 +690,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict_
 #pragma unroll
                 for (int e = 0; e < 8; ++e)
                     o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(xf[8 * j + e], rstd), nb), wf[e]), bf[e]);
-                if (m < M) *reinterpret_cast<uint4*>(xsb + m * GF_XS + lane * 8 + j * 512) = pack8(o);
+                *reinterpret_cast<uint4*>(xsb + m * GF_XS + lane * 8 + j * 512) = pack8(o);
             }
         }
         __syncthreads();
