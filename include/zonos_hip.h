@@ -23,6 +23,7 @@ extern "C" {
 int zk_version(void);                 /* ABI version (monotonic) */
 const char* zk_last_error(void);      /* thread-local message of the last failing call */
 int zk_device_sync(void);             /* hipDeviceSynchronize + error check */
+long zk_abi_size(int which);          /* sizeof / offsetof of the ABI structs (binding self-check) */
 
 /* ------------------------------------------------------------------ sampling
  * Mirrors sample_from_logits (zonos/sampling.py:232-328) incl.

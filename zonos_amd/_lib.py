@@ -124,12 +124,14 @@ def load():
     lib.zk_loudness_max_blocks.argtypes = [L, I]
     lib.zk_small_sync_words.restype = C.c_int
     lib.zk_small_sync_words.argtypes = [I]
+    lib.zk_abi_size.restype = C.c_long
+    lib.zk_abi_size.argtypes = [I]
     _lib = lib
     return lib
 
 
 def exported_symbols() -> list[str]:
-    return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_small_sync_words"]
+    return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_small_sync_words", "zk_abi_size"]
 
 
 def call(name: str, *args):
