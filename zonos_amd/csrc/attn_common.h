@@ -170,6 +170,42 @@ ZK_DEV void patch_kv(KVFrag& f, const uint32_t* s_kn, const uint16_t* s_vn, int 
 // release) and takes a ticket on cnt[row][kv head]; the workgroup drawing the last ticket of the
 // launch (tickets are monotonic: the count is a multiple of nsplit before every launch) acquires
 // and merges all nsplit partials exactly as k_attn_combine does. Saves the combine launch.
+// sum of the in_proj split-K slabs of one RoPE pair (d0, d1) of a column block, left to right
+// in fp32 like k_qkv_rope: every slab load issued before the first add
+template <int NS, bool NEOX>
+ZK_DEV void slab_pair(const float* p, size_t slab, int d0, int d1, float& a, float& b) {
+    float v0[NS], v1[NS];
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+        if constexpr (NEOX) {
+            v0[sl] = p[sl * slab + d0];
+            v1[sl] = p[sl * slab + d1];
+        } else {                                      // interleaved pair: d1 = d0 + 1, d0 even
+            const float2 t = *reinterpret_cast<const float2*>(p + sl * slab + d0);
+            v0[sl] = t.x;
+            v1[sl] = t.y;
+        }
+    }
+    a = v0[0];
+    b = v1[0];
+#pragma unroll
+    for (int sl = 1; sl < NS; ++sl) { a += v0[sl]; b += v1[sl]; }
+}
+ZK_DEV void slab_pair_n(const float* p, size_t slab, int ns, int d0, int d1, float& a, float& b) {
+    float v0[AT_MAXGS], v1[AT_MAXGS];
+#pragma unroll
+    for (int sl = 0; sl < AT_MAXGS; ++sl) {
+        const float* ps = p + (size_t)min(sl, ns - 1) * slab;
+        v0[sl] = ps[d0];
+        v1[sl] = ps[d1];
+    }
+    a = v0[0];
+    b = v1[0];
+#pragma unroll
+    for (int sl = 1; sl < AT_MAXGS; ++sl)
+        if (sl < ns) { a += v0[sl]; b += v1[sl]; }
+}
+
 // LDS of one attention workgroup (4 waves)
 struct __attribute__((aligned(16))) AttnSmem {
     float s_o[4][AT_G][128];
@@ -237,18 +273,16 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
             const int cb = hp < G ? (g * G + hp) * HD : (hp == G ? H * HD + g * HD : (H + Hkv) * HD + g * HD);
             // all slab loads issued together (clamped slab index, select after) -- same
             // left-to-right fp32 sum as k_qkv_rope
-            float v0[AT_MAXGS], v1[AT_MAXGS];
-#pragma unroll
-            for (int sl = 0; sl < AT_MAXGS; ++sl) {
-                const float* ps = prow + (size_t)min(sl, gsplit - 1) * slab + cb;
-                v0[sl] = ps[d0];
-                v1[sl] = ps[d1];
+            // the slab count is dispatched to an exact-size instantiation (B <= 8: 1 slab, c3: 4),
+            // so only real slabs are loaded (one 8-byte load per slab for the interleaved pair)
+            float a, bb;
+            switch (gsplit) {
+                case 1: slab_pair<1, NEOX>(prow + cb, slab, d0, d1, a, bb); break;
+                case 2: slab_pair<2, NEOX>(prow + cb, slab, d0, d1, a, bb); break;
+                case 4: slab_pair<4, NEOX>(prow + cb, slab, d0, d1, a, bb); break;
+                default: slab_pair_n(prow + cb, slab, gsplit, d0, d1, a, bb); break;
             }
             const float2 cs = *reinterpret_cast<const float2*>(fc + 2 * j);
-            float a = v0[0], bb = v1[0];
-#pragma unroll
-            for (int sl = 1; sl < AT_MAXGS; ++sl)
-                if (sl < gsplit) { a += v0[sl]; bb += v1[sl]; }
             a = round_bf(a);
             bb = round_bf(bb);
             if (hp <= G) {
