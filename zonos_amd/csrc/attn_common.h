@@ -206,6 +206,20 @@ ZK_DEV void slab_pair_n(const float* p, size_t slab, int ns, int d0, int d1, flo
         if (sl < ns) { a += v0[sl]; b += v1[sl]; }
 }
 
+// ZK_ATT_PROF (profiling builds only): thread 0 of each workgroup writes s_memrealtime stamps
+// [entry, loads issued, prologue done, key loop done, merged, end] to prof[wg * 8 + k].
+#ifdef ZK_ATT_PROF
+#define ZK_ATT_STAMP(k)                                                                                     \
+    do {                                                                                                    \
+        if (threadIdx.x == 0 && g_att_prof)                                                                 \
+            g_att_prof[((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + (k)] =          \
+                __builtin_amdgcn_s_memrealtime();                                                           \
+    } while (0)
+__device__ uint64_t* g_att_prof;
+#else
+#define ZK_ATT_STAMP(k) do {} while (0)
+#endif
+
 // LDS of one attention workgroup (4 waves)
 struct __attribute__((aligned(16))) AttnSmem {
     float s_o[4][AT_G][128];
@@ -235,6 +249,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
     auto& s_kn = sm.s_kn;
     auto& s_vn = sm.s_vn;
     auto& s_last = sm.s_last;
+    ZK_ATT_STAMP(0);
     const int nkb = (ctx + AT_KB - 1) / AT_KB;
     const int kb0 = (int)((long)split * nkb / nsplit), kb1 = (int)((long)(split + 1) * nkb / nsplit);
     const int G = H / Hkv;
@@ -258,6 +273,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
         load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
     }
     issued();
+    ZK_ATT_STAMP(1);
     if constexpr (FUSED) {
         // pairs: [0, G*64) q of heads g*G.., then 64 k pairs, then 64 v pairs
         const int N = (H + 2 * Hkv) * HD;
@@ -318,6 +334,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
             qf[ks] = as_frag(v);
         }
     }
+    ZK_ATT_STAMP(2);
     AttnState st;
     st.m = -INFINITY;
     st.l = 0.f;
@@ -337,6 +354,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
             }
         }
     }
+    ZK_ATT_STAMP(3);
     if (FUSED && split == nsplit - 1) {      // the split owning the newest key stores it (cache for later steps)
         const int t = threadIdx.x;
         if (t < HD / 2) *reinterpret_cast<uint32_t*>(kb + k_off(pos, t >> 2) + ((2 * t) & 7)) = s_kn[t];
@@ -354,6 +372,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
             for (int i = 0; i < 4; ++i) s_o[w][ln][dt * 16 + lg * 4 + i] = st.o[dt][i] * cw;
     }
     bar();
+    ZK_ATT_STAMP(4);
     if (nsplit == 1) {
         // normalised output for the G heads: thread -> (head, 2 channels)
         for (int i = threadIdx.x; i < G * HD / 2; i += 256) {
@@ -368,6 +387,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
             *reinterpret_cast<uint32_t*>(out + (size_t)r * H * HD + (size_t)(g * G + h) * HD + d) =
                 pack2(o0 * inv, o1 * inv);
         }
+        ZK_ATT_STAMP(5);
         return;
     }
     float* wp = work + (((size_t)r * Hkv + g) * nsplit + split) * AT_STR;
@@ -395,12 +415,14 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
             s_last = ((old + 1) % (uint32_t)nsplit) == 0;
         }
         bar();
+        ZK_ATT_STAMP(5);
         if (!s_last) return;
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
+        ZK_ATT_STAMP(6);
         const float* base = work + ((size_t)r * Hkv + g) * nsplit * AT_STR;
         for (int i = threadIdx.x; i < G * HD / 2; i += 256) {       // k_attn_combine's arithmetic
             const int j = i / (HD / 2), d = (i % (HD / 2)) * 2;
@@ -418,6 +440,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
             *reinterpret_cast<uint32_t*>(out + (size_t)r * H * HD + (size_t)(g * G + j) * HD + d) =
                 pack2(o0 * inv, o1 * inv);
         }
+        ZK_ATT_STAMP(7);
     }
 }
 

@@ -624,6 +624,12 @@ extern "C" int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const f
     return 0;
 }
 
+#ifdef ZK_ATT_PROF
+extern "C" int zk_att_prof_set(uint64_t* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_att_prof), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int zk_attn_prefill(const void* q, const void* k_cache, const void* vt_cache, int R, int S, int H,
                                int Hkv, int hd, int Smax, void* out, void* stream) {
     ZK_REQUIRE(hd == 128, "zk_attn_prefill: head_dim %d unsupported (128 only)", hd);
