@@ -25,7 +25,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr
-from .engine import ATTN_CHUNK, N_CB, VOCAB, HipDecoder, _split_for, attn_splits_for, pack_weights
+from .engine import ATTN_CHUNK, N_CB, VOCAB, HipDecoder, _split_for, _split_overrides, attn_splits_for, pack_weights
 
 
 @dataclass
@@ -176,8 +176,12 @@ class HybridDecoder(HipDecoder):
         Nh = N_CB * VOCAB
         Mp = R * S_pre
         f32, bf, i32 = torch.float32, torch.bfloat16, torch.int32
-        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R), fc2=_split_for(D, max(Fd, 64), R),
-                      heads=_split_for(Nh, D, R), inp=min(_split_for(nin, D, R), 8), out=_split_for(D, di, R))
+        # Mamba in_proj (N = 8512, K = 2048) without split-K: 133 workgroups, no fp32 slab round trip
+        # for k_mamba_step (c5 decode step 4.67 vs 4.87 ms with 2 splits, 4.96 with 4; tools/c5_split_ab.sh)
+        # (attention out_proj 4-way and the heads unsplit, as the transformer engine: 4.645 vs 4.670 ms)
+        splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R, target_blocks=128),
+                      fc2=_split_for(D, max(Fd, 64), R), heads=1, inp=1, out=_split_for(D, di, R))
+        splits.update(_split_overrides())
         part_n = max(Mp * Nqkv, Mp * D, Mp * nin, splits["qkv"] * R * Nqkv, splits["o"] * R * D,
                      splits["fc2"] * R * D, splits["heads"] * R * Nh, splits["inp"] * R * nin, splits["out"] * R * D)
         attn_splits = attn_splits_for(R, Hk, smax)
