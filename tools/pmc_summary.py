@@ -17,6 +17,7 @@ ap.add_argument("--match", default="k_attn_decode<true>")
 ap.add_argument("--R", type=int, default=128)
 ap.add_argument("--ctx", type=int, default=1705)
 ap.add_argument("--alg", type=float, default=0)
+ap.add_argument("--key", action="append", default=[], help="extra shape key=value (int) recorded in the JSON")
 a = ap.parse_args()
 
 acc = defaultdict(list)
@@ -41,5 +42,10 @@ if a.json and per:
                hbm_bytes_per_launch=tot, algorithmic_bytes_per_launch=a.alg,
                ratio=(tot / a.alg if a.alg else None),
                method="rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH_SIZE x2 (gfx950)")
+    for kv in a.key:
+        k, v = kv.split("=")
+        out[k] = int(v)
+    if a.ctx <= 0:
+        out.pop("ctx")
     json.dump(out, open(a.json, "w"), indent=1)
     print(json.dumps(out))
