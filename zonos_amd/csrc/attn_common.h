@@ -40,6 +40,9 @@ ZK_DEV void rope_dims(int j, int hd, int& d0, int& d1) {
 }
 
 // ------------------------------------------------------------------ decode attention
+#ifndef ZK_ATT_TRIM
+#define ZK_ATT_TRIM 1      // per-wave key-slice trimming (0: whole 128-key blocks, clamped tail load)
+#endif
 constexpr int AT_KB = 128;      // keys per workgroup iteration (4 waves x 32)
 constexpr int AT_G = 4;         // query heads per KV head handled by the B operand (<= 16)
 constexpr int AT_STR = 2 * AT_G + AT_G * 128;   // work floats per (r, g, split)
@@ -260,17 +263,27 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
 
     bf16x8 qf[4];
     KVFrag fa, fb;
-    const int last = kb1 - 1;
+#if ZK_ATT_TRIM
+    // This wave's 32-key slice of block b holds keys b*128 + 32w ..: it loads and multiplies only
+    // the blocks whose slice holds a visible key (b*128 + 32w < ctx) and never re-loads the last
+    // one. (Reading whole 128-key blocks plus a clamped tail prefetch fetched 11 % more than the
+    // algorithmic bytes at ctx 1705; a fully masked slice adds exactly nothing to (m, l, O).)
+    const int vis = ctx - 32 * w;
+    const int kbw = vis <= 0 ? kb0 : max(kb0, min(kb1, (vis + AT_KB - 1) / AT_KB));
+#else
+    const int kbw = kb1;
+#endif
+    const int last = kbw - 1;
     // the first key block can be fetched before the prologue unless it holds the new key
     // FUSED: the new key's cache lines are written only at the end of the kernel (a store
     // followed by loads of the same partially written lines stalls the key loop); the key loop
     // patches the new K/V into its registers from LDS instead, so the arithmetic is exactly
     // that of reading the cache. The first key block can therefore be fetched before the prologue.
     const int pos = ctx - 1;
-    const bool early = FUSED && kb1 > kb0;
+    const bool early = FUSED && kbw > kb0;
     if (early) {      // the first TWO key blocks are in flight during the prologue
         load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
-        load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
+        if (!ZK_ATT_TRIM || kb0 + 1 < kbw) load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
     }
     issued();
     ZK_ATT_STAMP(1);
@@ -341,14 +354,15 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if (kb1 > kb0) {
+    if (kbw > kb0) {
         if (!early) load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
-        for (int it = kb0; it < kb1; it += 2) {
-            if (!(early && it == kb0)) load_kv<KVNT>(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
+        for (int it = kb0; it < kbw; it += 2) {
+            if (!(early && it == kb0) && (!ZK_ATT_TRIM || it + 1 < kbw))
+                load_kv<KVNT>(fb, kb, vb, Smax, min(it + 1, last) * AT_KB + 32 * w, ln, lg);
             if (FUSED) patch_kv(fa, s_kn, s_vn, it * AT_KB + 32 * w, pos, ln, lg);
             attn_step(st, fa, qf, it * AT_KB + 32 * w, ctx, scale, lg);
-            load_kv<KVNT>(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
-            if (it + 1 < kb1) {
+            if (!ZK_ATT_TRIM || it + 2 < kbw) load_kv<KVNT>(fa, kb, vb, Smax, min(it + 2, last) * AT_KB + 32 * w, ln, lg);
+            if (it + 1 < kbw) {
                 if (FUSED) patch_kv(fb, s_kn, s_vn, (it + 1) * AT_KB + 32 * w, pos, ln, lg);
                 attn_step(st, fb, qf, (it + 1) * AT_KB + 32 * w, ctx, scale, lg);
             }
