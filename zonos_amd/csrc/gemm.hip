@@ -249,6 +249,9 @@ constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 #ifndef ZK_SLAB_NT
 #define ZK_SLAB_NT 1
 #endif
+#ifndef ZK_WS_XCD
+#define ZK_WS_XCD 1                // k_gemm_ws: XCD-aware split-major tile order
+#endif
 #ifndef ZK_WS_EPI
 #define ZK_WS_EPI 1                // k_gemm_ws epilogue staged through LDS (whole-row stores)
 #endif
@@ -269,7 +272,21 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
                                                            bf16_t* __restrict__ Cout, const int32_t* skip) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip && *skip) return;
-    const int n0 = blockIdx.x * BN, split = blockIdx.z;
+    int bx = blockIdx.x, bz = blockIdx.z;
+#if ZK_WS_XCD
+    // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (linear id % 8),
+    // and every workgroup of one K split reads the same activation slice. Numbering the work
+    // split-major and handing each XCD a contiguous run of it puts one split (fc2: 8 splits) or
+    // half a split (in_proj / out_proj: 4) on each XCD, so its L2 fetches only that K slice of the
+    // activation instead of all of it. Placement only: every tile computes the same numbers.
+    if (gridDim.z > 1 && ((gridDim.x * gridDim.z) & 7) == 0) {
+        const int L = blockIdx.x + gridDim.x * blockIdx.z;               // gridDim.y == 1
+        const int I = (L & 7) * ((gridDim.x * gridDim.z) >> 3) + (L >> 3);
+        bz = I / gridDim.x;
+        bx = I - bz * gridDim.x;
+    }
+#endif
+    const int n0 = bx * BN, split = bz;
     const int kbeg = split * kslice;
     const int nchunks = kslice / BK;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
