@@ -106,6 +106,13 @@ int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, in
 int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, int mode,
                   const void* ln_w, const void* ln_b, float eps, float* Cf, void* Cb,
                   const int32_t* skip, void* stream);
+/* Attention out_proj of a small decode batch (M = 2B <= 2 rows) straight from the split
+ * partials of zk_attn_decode_qkv_part: x[M][N] = bf16(x + bf16(merge(work) . W^T))
+ * (_torch.py:66 + the residual add of :100), the merge being k_attn_combine's arithmetic
+ * (bit-identical to zk_attn_decode_qkv + zk_gemv_fused mode 2 with the same nsplit).
+ * K = 2048 (16 heads x 128), nsplit in {2, 4, 8}. */
+int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const void* W, int M, int N, int K,
+                     void* x, const int32_t* skip, void* stream);
 /* Persistent small-batch decode step (R = 2B <= 4 rows, Zonos-v0.1-transformer geometry:
  * D 2048, 16/4 heads x 128, FFN 8192): the whole backbone of one decode step
  * (zonos/backbone/_torch.py:99-102,117-152 for every layer, then norm_f and the 9 heads of
@@ -216,6 +223,15 @@ int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const float* freqs
                           void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
                           const int32_t* ctx_dev, float* work, int nsplit, uint32_t* counters, void* out,
                           int rope_neox, const int32_t* skip, void* stream);
+
+/* zk_attn_decode_qkv for nsplit >= 2 key ranges WITHOUT the merge: leaves the split partials
+ * (m, l, unnormalised O per query head) in work [R][Hkv][nsplit][8 + 4*128] fp32 for the
+ * consumer, zk_gemv_attn_out, which merges them in its prologue (replaces the
+ * F.scaled_dot_product_attention output of _torch.py:64-65 feeding out_proj, :66). */
+int zk_attn_decode_qkv_part(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
+                            void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
+                            const int32_t* ctx_dev, float* work, int nsplit, int rope_neox,
+                            const int32_t* skip, void* stream);
 
 /* ------------------------------------------------------------------ graphs and timing
  * The decode step is captured once into a hipGraph and replayed (the reference runs the

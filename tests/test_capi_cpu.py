@@ -62,7 +62,9 @@ def test_split_selection_batch_invariant():
 def test_attention_split_rule():
     """Flash-decoding key splits: none at B=64 (512 workgroups already), and each split covers
     >= 2048 cached keys (a combine launch costs more than it saves below that)."""
-    from zonos_amd.engine import attn_splits_for
+    from zonos_amd.engine import attn_merge_for, attn_splits_for
+    assert attn_merge_for(2, 1280) == 4 and attn_merge_for(2, 256) == 2 and attn_merge_for(2, 128) == 0
+    assert attn_merge_for(4, 1280) == 0 and attn_merge_for(128, 3072) == 0
     assert attn_splits_for(128, 4, 3072) == 1           # c3
     assert attn_splits_for(2, 4, 1280) == 1             # c2: B=1, 10 s
     assert attn_splits_for(2, 4, 3328) == 2             # B=1, 30 s

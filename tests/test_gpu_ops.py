@@ -381,3 +381,41 @@ def test_attention_split_combine_in_launch(R, ctx, nsplit):
         assert torch.equal(out, ref), (rep, (out.float() - ref.float()).abs().max())
         assert torch.equal(kc, kc2) and torch.equal(vt, vt2)
     assert bool((cnt.cpu() % nsplit == 0).all()) and int(cnt.cpu()[0]) == 3 * nsplit
+
+
+@pytest.mark.parametrize("R,ctx,nsplit", [(2, 300, 2), (2, 700, 4), (2, 1000, 8), (1, 129, 2), (2, 161, 8)])
+def test_attention_out_proj_merge(R, ctx, nsplit):
+    """zk_attn_decode_qkv_part + zk_gemv_attn_out (the split partials merged in the out_proj
+    GEMV's prologue) == zk_attn_decode_qkv (+ k_attn_combine) + zk_gemv_fused mode 2, bit for
+    bit: the residual stream after out_proj and the KV cache contents."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import pack_weights, rope_table
+    H, Hk, hd, D = 16, 4, 128, 2048
+    smax = ((ctx + 255) // 256) * 256
+    nsplit = min(nsplit, smax // 128)
+    g = torch.Generator(device="cpu").manual_seed(ctx * 7 + nsplit)
+    kc = torch.randn(R * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    vt = torch.randn(R * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    part = (torch.randn(R * (H + 2 * Hk) * hd, generator=g) * 0.5).to(DEV)
+    freqs = rope_table(16384, hd).to(DEV)
+    s = stream_ptr()
+    Wo = pack_weights((torch.randn(D, H * hd, generator=g) * 0.02).to(torch.bfloat16).to(DEV), s)
+    x0 = torch.randn(R, D, generator=g).to(torch.bfloat16).to(DEV)
+    # reference sequence: attention output (split + combine launch), then out_proj + residual
+    kc1, vt1, x1 = kc.clone(), vt.clone(), x0.clone()
+    work1 = torch.empty(R * Hk * nsplit * (8 + 4 * hd), device=DEV)
+    y = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
+    call("zk_attn_decode_qkv", ptr(part), 1, ptr(freqs), ptr(kc1), ptr(vt1), R, H, Hk, hd, smax, ctx, None,
+         ptr(work1), nsplit, ptr(y), 0, None, s)
+    call("zk_gemv_fused", ptr(y), H * hd, ptr(Wo), R, D, H * hd, 2, None, None, 1e-5, None, ptr(x1), None, s)
+    # merged in the consumer
+    kc2, vt2, x2 = kc.clone(), vt.clone(), x0.clone()
+    work2 = torch.full((R * Hk * nsplit * (8 + 4 * hd),), float("nan"), device=DEV)
+    call("zk_attn_decode_qkv_part", ptr(part), 1, ptr(freqs), ptr(kc2), ptr(vt2), R, H, Hk, hd, smax, ctx, None,
+         ptr(work2), nsplit, 0, None, s)
+    call("zk_gemv_attn_out", ptr(work2), nsplit, Hk, ptr(Wo), R, D, H * hd, ptr(x2), None, s)
+    torch.cuda.synchronize()
+    assert torch.equal(kc1, kc2) and torch.equal(vt1, vt2)
+    assert torch.equal(x1.view(torch.int16), x2.view(torch.int16)), (x1.float() - x2.float()).abs().max()
+    # and the result is the attention + projection of an fp32 reference within bf16 tolerance
+    assert not torch.equal(x1, x0)

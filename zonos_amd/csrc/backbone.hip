@@ -598,6 +598,29 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
     return 0;
 }
 
+extern "C" int zk_attn_decode_qkv_part(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
+                                       void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
+                                       const int32_t* ctx_dev, float* work, int nsplit, int rope_neox,
+                                       const int32_t* skip, void* stream) {
+    ZK_REQUIRE(hd == 128, "zk_attn_decode_qkv_part: head_dim %d unsupported (128 only)", hd);
+    ZK_REQUIRE(H % Hkv == 0 && H / Hkv <= AT_G, "zk_attn_decode_qkv_part: GQA group %d > %d", H / Hkv, AT_G);
+    ZK_REQUIRE(Smax % AT_KB == 0, "zk_attn_decode_qkv_part: Smax=%d must be a multiple of %d", Smax, AT_KB);
+    ZK_REQUIRE(nsplit >= 2 && nsplit <= Smax / AT_KB, "zk_attn_decode_qkv_part: nsplit=%d out of [2, %d]", nsplit,
+               Smax / AT_KB);
+    ZK_REQUIRE(work != nullptr, "zk_attn_decode_qkv_part: null work buffer");
+    ZK_REQUIRE(part != nullptr && freqs != nullptr && gemm_nsplit >= 1 && gemm_nsplit <= AT_MAXGS,
+               "zk_attn_decode_qkv_part: bad arguments (gemm_nsplit=%d, max %d)", gemm_nsplit, AT_MAXGS);
+    const float scale = 1.0f / sqrtf((float)hd);
+    const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
+    auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true> : k_attn_decode<true, true, false>)
+                          : (kvnt ? k_attn_decode<true, false, true> : k_attn_decode<true, false, false>);
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
+                       (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, nullptr, skip, part,
+                       gemm_nsplit, freqs, nullptr);
+    ZK_CHECK_LAUNCH("zk_attn_decode_qkv_part");
+    return 0;
+}
+
 extern "C" int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
                                      void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
                                      const int32_t* ctx_dev, float* work, int nsplit, uint32_t* counters, void* out,

@@ -249,6 +249,9 @@ constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 #ifndef ZK_SLAB_NT
 #define ZK_SLAB_NT 1
 #endif
+#ifndef ZK_SLAB_SC1
+#define ZK_SLAB_SC1 0              // write-through (sc1) slab stores: nothing left dirty in L2 at the boundary
+#endif
 #ifndef ZK_WS_XCD
 #define ZK_WS_XCD 1                // k_gemm_ws: XCD-aware split-major tile order
 #endif
@@ -424,7 +427,9 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
                     const f32x4 v = *reinterpret_cast<const f32x4*>(tile + m * TS + c4);
                     float* dst = C + (size_t)m * N + n0 + c4;
                     if (n0 + c4 + 3 < N) {
-                        if constexpr (ZK_SLAB_NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+                        if constexpr (ZK_SLAB_SC1)
+                            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+                        else if constexpr (ZK_SLAB_NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
                         else *reinterpret_cast<f32x4*>(dst) = v;
                     } else {
                         for (int e = 0; e < 4 && n0 + c4 + e < N; ++e) dst[e] = v[e];
@@ -592,20 +597,28 @@ constexpr int GF_XS = 2048 + 8;    // LDS row stride (bf16) of the LayerNorm'd r
 // read k-step 2j+1 at their neighbour's position (lane ^ 8); a DPP row rotation by 8 then moves
 // the k-step 2j+1 values to the owning lanes for the second MFMA. The other half's output
 // columns are garbage and never stored.
-template <int MODE, bool LN, int NTW, bool HALF, int NW, int KS, int PF>
+// MRG (0, 2, 4, 8): the activation is the decode attention's output, still split over MRG key
+// ranges -- the [row][kv head][split] (m, l, O) partials of zk_attn_decode_qkv_part in `mw` --
+// and the prologue merges them exactly as k_attn_combine does (backbone.hip) into LDS; each
+// wave merges the 2 heads of its own K range (K = 2048, NW = 8), rows < M <= 2.
+constexpr int GF_AT_G = 4, GF_AT_STR = 2 * GF_AT_G + GF_AT_G * 128;    // = AT_G, AT_STR (attn_common.h)
+template <int MODE, bool LN, int NTW, bool HALF, int NW, int KS, int PF, int MRG = 0>
 __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict__ A, long lda,
                                                        const bf16_t* __restrict__ W, int M, int N, int K,
                                                        const bf16_t* __restrict__ lnw, const bf16_t* __restrict__ lnb,
                                                        float eps, float* __restrict__ Cf, bf16_t* __restrict__ Cb,
-                                                       const int32_t* skip) {
+                                                       const int32_t* skip, const float* __restrict__ mw = nullptr,
+                                                       int mhkv = 1) {
     static_assert(!HALF || NTW == 1, "HALF is one half tile");
     static_assert(!LN || KS * NW * 32 == 2048, "LN prologue: K = 2048");
+    static_assert(!MRG || (!LN && NW == 8 && KS * NW * 32 == 2048), "merge prologue: K = 2048, 8 waves");
     static_assert(NTW <= NW, "one finishing wave per tile");
+    constexpr bool XS = LN || MRG;                                   // activation from LDS
     constexpr int KPL = HALF ? 2 : 1;                                // k-steps per weight load
     constexpr int NL = KS / KPL;                                     // weight loads per wave and tile
     static_assert(NL * KPL == KS, "HALF pairs k-steps");
     constexpr int MR = 16 / NW;                                      // LN rows per wave
-    __shared__ __attribute__((aligned(16))) uint4 xs[LN ? 16 * GF_XS / 8 : 1];
+    __shared__ __attribute__((aligned(16))) uint4 xs[XS ? 16 * GF_XS / 8 : 1];
     __shared__ __attribute__((aligned(16))) f32x4 red[NW][NTW][64];
     if (skip && *skip) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -635,6 +648,27 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict_
             for (int j = 0; j < NJ; ++j)
                 xv[rr][j] = *reinterpret_cast<const uint4*>(A + (size_t)min(w + NW * rr, M - 1) * lda + lane * 8 + j * 512);
     }
+    // MRG: lane item i = (row i >> 1, dim pair lane + 64 (i & 1)) of this wave's 256 dims
+    // (2 heads): every split's (m, l, O pair) loaded here, merged after the weight prefetch
+    constexpr int NS = MRG ? MRG : 1;
+    float mm[MRG ? 4 : 1][NS], ml[MRG ? 4 : 1][NS];
+    float2 mo[MRG ? 4 : 1][NS];
+    if constexpr (MRG) {
+        const int G = (K >> 7) / mhkv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = min(i >> 1, M - 1);
+            const int k = kbeg + 2 * (lane + 64 * (i & 1));
+            const int h = k >> 7, d = k & 127, g = h / G, j = h - g * G;
+            const float* base = mw + ((size_t)m * mhkv + g) * MRG * GF_AT_STR;
+#pragma unroll
+            for (int sp = 0; sp < NS; ++sp) {
+                mm[i][sp] = base[sp * GF_AT_STR + j];
+                ml[i][sp] = base[sp * GF_AT_STR + GF_AT_G + j];
+                mo[i][sp] = *reinterpret_cast<const float2*>(base + sp * GF_AT_STR + 2 * GF_AT_G + j * 128 + d);
+            }
+        }
+    }
     bf16_t rv[4] = {0, 0, 0, 0};                                     // residual x of the epilogue
     const int t = w;                                                 // wave w finishes tile w
     const int n_out = (nt0 + t) * 16 + ln;
@@ -658,7 +692,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict_
     auto issue = [&](int ls, int slot) {
 #pragma unroll
         for (int tt = 0; tt < NTW; ++tt) wr[slot][tt] = ldg_w<true>(wp[tt] + ls * 512 * KPL);
-        if constexpr (!LN) {
+        if constexpr (!XS) {
 #pragma unroll
             for (int q = 0; q < KPL; ++q) ar[slot][q] = *reinterpret_cast<const uint4*>(ap + (ls * KPL + q) * 32);
         }
@@ -712,6 +746,38 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict_
         }
         __syncthreads();
     }
+    if constexpr (MRG) {
+        // k_attn_combine's arithmetic, split by split in order (fp32, no contraction)
+        uint32_t* xsw = reinterpret_cast<uint32_t*>(xs);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int sp = 0; sp < NS; ++sp) {
+                u32x4 t = {__float_as_uint(mm[i][sp]), __float_as_uint(ml[i][sp]), __float_as_uint(mo[i][sp].x),
+                           __float_as_uint(mo[i][sp].y)};
+                asm volatile("" : "+v"(t));               // no merge arithmetic above the weight prefetch
+                mm[i][sp] = __uint_as_float(t[0]);
+                ml[i][sp] = __uint_as_float(t[1]);
+                mo[i][sp] = make_float2(__uint_as_float(t[2]), __uint_as_float(t[3]));
+            }
+            float Mx = -INFINITY;
+#pragma unroll
+            for (int sp = 0; sp < NS; ++sp) Mx = fmaxf(Mx, mm[i][sp]);
+            float L = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+            for (int sp = 0; sp < NS; ++sp) {
+                const float c = (mm[i][sp] == -INFINITY) ? 0.f : __expf(mm[i][sp] - Mx);
+                L += ml[i][sp] * c;
+                o0 += mo[i][sp].x * c;
+                o1 += mo[i][sp].y * c;
+            }
+            const float inv = 1.0f / L;
+            const int m = i >> 1;
+            const int k = kbeg + 2 * (lane + 64 * (i & 1));
+            if (m < M) xsw[(m * GF_XS + k) >> 1] = pack2(o0 * inv, o1 * inv);
+        }
+        // each wave reads back only the dims it wrote (its own K range): no workgroup barrier
+    }
 
     f32x4 acc[NTW];
 #pragma unroll
@@ -724,7 +790,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict_
 #pragma unroll
         for (int q = 0; q < KPL; ++q) {
             uint4 a;
-            if constexpr (LN) a = *reinterpret_cast<const uint4*>(xrow + (ls * KPL + q) * 32);
+            if constexpr (XS) a = *reinterpret_cast<const uint4*>(xrow + (ls * KPL + q) * 32);
             else a = ar[ls % U][q];
 #pragma unroll
             for (int tt = 0; tt < NTW; ++tt) {
@@ -1011,6 +1077,28 @@ extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int 
 #undef ZK_GF
     ZK_REQUIRE(handled, "zk_gemv_fused: no kernel for K=%d", K);
     ZK_CHECK_LAUNCH("zk_gemv_fused");
+    return 0;
+}
+
+extern "C" int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const void* W, int M, int N, int K,
+                                void* x, const int32_t* skip_flag, void* stream) {
+    ZK_REQUIRE(M >= 1 && M <= 2, "zk_gemv_attn_out: M=%d (1..2)", M);
+    ZK_REQUIRE(K == 2048 && N > 0 && N % 16 == 0, "zk_gemv_attn_out: K=%d (2048) N=%d", K, N);
+    ZK_REQUIRE(Hkv >= 1 && (K / 128) % Hkv == 0 && (K / 128) / Hkv <= GF_AT_G, "zk_gemv_attn_out: Hkv=%d", Hkv);
+    ZK_REQUIRE(work != nullptr && x != nullptr, "zk_gemv_attn_out: null buffer");
+    const int grid = 2 * ((N + 15) / 16);                   // half tiles, 8 K-range waves
+#define ZK_GAO(NS_)                                                                                              \
+    hipLaunchKernelGGL((k_gemv_f<2, false, 1, true, 8, 8, 4, NS_>), dim3(grid), dim3(512), 0,                  \
+                       (hipStream_t)stream, reinterpret_cast<const bf16_t*>(work), (long)K, (const bf16_t*)W, M,  \
+                       N, K, nullptr, nullptr, 0.f, nullptr, (bf16_t*)x, skip_flag, work, Hkv)
+    switch (nsplit) {
+        case 2: ZK_GAO(2); break;
+        case 4: ZK_GAO(4); break;
+        case 8: ZK_GAO(8); break;
+        default: ZK_REQUIRE(false, "zk_gemv_attn_out: nsplit=%d (2, 4 or 8)", nsplit);
+    }
+#undef ZK_GAO
+    ZK_CHECK_LAUNCH("zk_gemv_attn_out");
     return 0;
 }
 

@@ -103,6 +103,28 @@ def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> in
     return max(1, min(want, cap, smax // 128))
 
 
+def attn_merge_for(R: int, smax: int) -> int:
+    """B = 1 (R = 2 rows): key splits of the decode attention whose partials the out_proj GEMV
+    merges in its prologue (zk_attn_decode_qkv_part + zk_gemv_attn_out) -- more CUs stream the
+    small KV cache without a combine launch or in-launch tickets. 0 = unsplit attention."""
+    if R > 2:
+        return 0
+    env = os.environ.get("ZK_ATTN_MERGE")          # tuning knob
+    if env is None and os.environ.get("ZK_ATTN_SPLITS"):
+        return 0                                    # an explicit split count selects the other forms
+    n = int(env) if env else ATTN_MERGE_DEFAULT
+    n = min(n, smax // 128)
+    for v in (8, 4, 2):
+        if n >= v:
+            return v
+    return 0
+
+
+# c2 (B=1, Lc=160, 861 tokens) decode step: 1.13 ms unsplit, 1.09 / 1.07 / 1.085 ms with 2 / 4 / 8
+# merged splits (profiles/r2_s4_attn_merge_ab.txt)
+ATTN_MERGE_DEFAULT = 4
+
+
 class HipBackbone:
     """The 26 transformer blocks + final LayerNorm on the device (zonos/backbone/_torch.py:52-152):
     bf16 weights in the engine's layouts and the layer launch sequence. Shared by the generate()
@@ -149,15 +171,22 @@ class HipBackbone:
         D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
         Nqkv = (H + 2 * Hk) * hd
         x, y, h, part, scal = ws["x"], ws["y"], ws["h"], ws["part"], ws["scal"]
+        merge = ws.get("attn_merge", 0)
         for i, L in enumerate(self.layers):
             kc, vt = self._kv(ws, i)
             call("zk_gemv_fused", ptr(x), D, ptr(L["wqkv"]), R, Nqkv, D, 0, ptr(L["ln1_w"]), ptr(L["ln1_b"]), c.eps,
                  ptr(part), None, skip, stream)
-            call("zk_attn_decode_qkv_sc", ptr(part), 1, ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"],
-                 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["attn_cnt"]), ptr(y),
-                 self.rope_neox, skip, stream)
-            call("zk_gemv_fused", ptr(y), H * hd, ptr(L["wo"]), R, D, H * hd, 2, None, None, c.eps, None, ptr(x),
-                 skip, stream)
+            if merge:
+                call("zk_attn_decode_qkv_part", ptr(part), 1, ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), merge, self.rope_neox, skip, stream)
+                call("zk_gemv_attn_out", ptr(ws["attn_work"]), merge, Hk, ptr(L["wo"]), R, D, H * hd, ptr(x), skip,
+                     stream)
+            else:
+                call("zk_attn_decode_qkv_sc", ptr(part), 1, ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                     ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["attn_cnt"]),
+                     ptr(y), self.rope_neox, skip, stream)
+                call("zk_gemv_fused", ptr(y), H * hd, ptr(L["wo"]), R, D, H * hd, 2, None, None, c.eps, None,
+                     ptr(x), skip, stream)
             call("zk_gemv_fused", ptr(x), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, ptr(L["ln2_w"]), ptr(L["ln2_b"]),
                  c.eps, None, ptr(h), skip, stream)
             call("zk_gemv_fused", ptr(h), Fd, ptr(L["fc2"]), R, D, Fd, 2, None, None, c.eps, None, ptr(x), skip,
@@ -276,13 +305,16 @@ class HipDecoder(HipBackbone):
         part_n = max(Mp * Nqkv, Mp * D, splits["qkv"] * R * Nqkv, splits["o"] * R * D, splits["fc2"] * R * D,
                      splits["heads"] * R * Nh)
         attn_splits = attn_splits_for(R, Hk, smax)
+        attn_merge = attn_merge_for(R, smax)
         ws = dict(
             key=key, R=R, T=T, Ld=Ld, smax=smax, S_pre=S_pre, splits=splits, attn_splits=attn_splits,
+            attn_merge=attn_merge,
             kv=torch.zeros(c.n_layer, 2, R * Hk * smax * hd, dtype=bf, device=dev),
             x=torch.empty(Mp, D, dtype=bf, device=dev), xn=torch.empty(Mp, D, dtype=bf, device=dev),
             q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
             h=torch.empty(Mp, Fd, dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
-            attn_work=torch.empty(max(1, R * Hk * attn_splits * (8 + 4 * hd)), dtype=f32, device=dev),
+            attn_work=torch.empty(max(1, R * Hk * max(attn_splits, attn_merge) * (8 + 4 * hd)), dtype=f32,
+                                  device=dev),
             attn_cnt=torch.zeros(R * Hk, dtype=i32, device=dev),     # in-launch split-combine tickets
             scal=torch.zeros(16, dtype=i32, device=dev),
             eos_mode=torch.zeros(B, dtype=i32, device=dev), steps_after=torch.zeros(B, dtype=i32, device=dev),
