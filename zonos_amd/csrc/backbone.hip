@@ -224,6 +224,8 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
 // t + 256 of the row, so every fp32 slab load instruction of a wave reads 1 KB contiguous (the
 // 8-element-per-thread layout of k_resid_ln reads 16 B of every 32 B per instruction, each
 // line twice). Same arithmetic per element; the LayerNorm sums group the elements differently.
+// NS > 0: exactly NS slabs (only real slabs loaded); NS = 0: nsplit <= RL_MAXS with clamped loads
+template <int NS>
 __global__ __launch_bounds__(LN_NT) void k_resid_ln_d2k(const float* part, int nsplit, const bf16_t* x_in,
                                                         const bf16_t* w, const bf16_t* b, float eps, int rows,
                                                         bf16_t* x_out, bf16_t* xn_out, int ln_on_sum,
@@ -240,17 +242,18 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln_d2k(const float* part, int n
     const uint2 x0 = *reinterpret_cast<const uint2*>(x_in + (size_t)row * D + c0);
     const uint2 x1 = *reinterpret_cast<const uint2*>(x_in + (size_t)row * D + c1);
     const float* p = part + (size_t)row * D;
-    float4 a0[RL_MAXS], a1[RL_MAXS];
+    constexpr int NL = NS ? NS : RL_MAXS;
+    float4 a0[NL], a1[NL];
 #pragma unroll
-    for (int sp = 0; sp < RL_MAXS; ++sp) {
-        const float* ps = p + (size_t)min(sp, nsplit - 1) * slab;
+    for (int sp = 0; sp < NL; ++sp) {
+        const float* ps = p + (size_t)(NS ? sp : min(sp, nsplit - 1)) * slab;
         a0[sp] = *reinterpret_cast<const float4*>(ps + c0);
         a1[sp] = *reinterpret_cast<const float4*>(ps + c1);
     }
     float acc[8] = {a0[0].x, a0[0].y, a0[0].z, a0[0].w, a1[0].x, a1[0].y, a1[0].z, a1[0].w};
 #pragma unroll
-    for (int sp = 1; sp < RL_MAXS; ++sp)
-        if (sp < nsplit) {
+    for (int sp = 1; sp < NL; ++sp)
+        if (NS || sp < nsplit) {
             acc[0] += a0[sp].x; acc[1] += a0[sp].y; acc[2] += a0[sp].z; acc[3] += a0[sp].w;
             acc[4] += a1[sp].x; acc[5] += a1[sp].y; acc[6] += a1[sp].z; acc[7] += a1[sp].w;
         }
@@ -511,7 +514,10 @@ extern "C" int zk_resid_ln(const float* part, int nsplit, const void* x_in, cons
         return !(e && e[0] == '0');
     }();
     if (D == 2048 && nsplit <= RL_MAXS && d2k) {
-        hipLaunchKernelGGL(k_resid_ln_d2k, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, part, nsplit,
+        // exact-size instantiations for the split counts the engine uses (fewer load instructions)
+        auto kern = nsplit == 1 ? k_resid_ln_d2k<1> : nsplit == 2 ? k_resid_ln_d2k<2> : nsplit == 4 ? k_resid_ln_d2k<4>
+                  : nsplit == 8 ? k_resid_ln_d2k<8> : k_resid_ln_d2k<0>;
+        hipLaunchKernelGGL(kern, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, part, nsplit,
                            (const bf16_t*)x_in, (const bf16_t*)w, (const bf16_t*)b, eps, rows, (bf16_t*)x_out,
                            (bf16_t*)xn_out, ln_on_sum, skip);
         ZK_CHECK_LAUNCH("zk_resid_ln");
