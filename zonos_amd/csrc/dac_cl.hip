@@ -80,6 +80,10 @@ ZK_DEV void wait_vm(int n) {
 
 constexpr int CL_DA = 3;                 // weight slices in flight ahead of the step being computed
 constexpr int CL_NW = CL_DA + 2;         // weight ring slots
+#ifndef ZK_CL_DEEP_DA
+#define ZK_CL_DEEP_DA 8
+#endif
+constexpr int CL_DEEP_DA = ZK_CL_DEEP_DA; // deep form: weight slices in flight
 constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 
 // Loader-wave implicit GEMM. Wave 4 only moves bytes (LDS-DMA) and counts its own vmcnt;
@@ -87,8 +91,10 @@ constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 // (it cannot tell the DMA's LDS range) costs nothing -- they have no loads in flight.
 // Step i = (chunk c, tap t); the loader runs CL_DA steps ahead for weights and DX steps
 // ahead for windows (DX >= CL_DA, window ring of NX slots), one raw s_barrier per step.
-template <int FM, bool SF32, bool RES, int NQ>
-__global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
+// DA: weight slices the loader keeps in flight (ring of DA + 2 slots); OCC: workgroups per CU the
+// registers are sized for (the deep form runs one workgroup per CU with a 2.7x deeper weight ring)
+template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2>
+__global__ __launch_bounds__(CL_THREADS, OCC) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
     int out_off0, int Tout, const float* resid, float* xout, const float* __restrict__ alpha,
@@ -117,7 +123,7 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
     const int nxp = (win + 15) >> 4;             // window pieces (16 rows each)
     const int XS = nxp * 1024;
     char* const wring = smem;
-    char* const xring = smem + CL_NW * WS;
+    char* const xring = smem + (DA + 2) * WS;
     const int nchunk = Cin / CI, nstep = nchunk * ks;
 
     if (wv == 4) {
@@ -128,10 +134,10 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
         const uint16_t* inb = in + (size_t)b * Tin * Cin;
         const int u0 = q0 - pad;
         const int prow = lane >> 2, pslot = lane & 3;   // a 1 KiB piece = 16 rows x 4 slots
-        int hist[CL_DA + 1] = {};                       // loads issued by iterations j-CL_DA .. j
+        int hist[DA + 1] = {};                       // loads issued by iterations j-DA .. j
         for (int j = -dx; j < nstep; ++j) {
             int nl = 0;
-            // window first: a window issued in the same iteration as W(j+CL_DA) is then older
+            // window first: a window issued in the same iteration as W(j+DA) is then older
             // than it, so waiting for W(j) below also covers every window step j can need
             const int sx = j + dx;
             if (sx >= 0 && sx < nstep && sx % ks == 0) {
@@ -148,10 +154,10 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
                 }
                 nl += nxp;
             }
-            const int sw = j + CL_DA;
+            const int sw = j + DA;
             if (sw >= 0 && sw < nstep) {
                 const int c = sw / ks, t = sw - c * ks;
-                char* dst = wring + (sw % CL_NW) * WS;
+                char* dst = wring + (sw % (DA + 2)) * WS;
                 const uint16_t* src0 = wp + t * wtap + (size_t)co0 * Cin + c * CI;
 #pragma unroll
                 for (int p = 0; p < NWP; ++p) {
@@ -163,13 +169,13 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
                 nl += NWP;
             }
 #pragma unroll
-            for (int k = 0; k < CL_DA; ++k) hist[k] = hist[k + 1];
-            hist[CL_DA] = nl;
+            for (int k = 0; k < DA; ++k) hist[k] = hist[k + 1];
+            hist[DA] = nl;
             if (j >= 0) {
-                // step j needs W(j), issued by iteration j - CL_DA; everything issued later may stay in flight
+                // step j needs W(j), issued by iteration j - DA; everything issued later may stay in flight
                 int pend = 0;
 #pragma unroll
-                for (int k = 1; k <= CL_DA; ++k) pend += hist[k];
+                for (int k = 1; k <= DA; ++k) pend += hist[k];
                 wait_vm(pend);
                 __builtin_amdgcn_s_barrier();           // publish step j
             }
@@ -207,7 +213,7 @@ __global__ __launch_bounds__(CL_THREADS, 2) void k_conv_cl(
         __builtin_amdgcn_s_barrier();            // step s is in LDS
         asm volatile("" ::: "memory");
         const char* xb = xring + (c % nx_slots) * XS;
-        const char* wb = wring + (s % CL_NW) * WS;
+        const char* wb = wring + (s % (DA + 2)) * WS;
         uint4 a[FM], bq[NQ];
 #pragma unroll
         for (int m = 0; m < FM; ++m)
@@ -450,13 +456,22 @@ bool dac_wide_enabled() {
     return on;
 }
 
-template <int FM, int NQ>
+// ZK_DAC_DEEP=1: plain k7 convs in the deep form (A/B knob, read once; default off)
+bool dac_deep_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("ZK_DAC_DEEP");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+template <int FM, int NQ, int DA = CL_DA, int OCC = 2>
 void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Cin, int Tin, const uint16_t* w,
                  long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
                  int out_stride, int out_off0, int Tout, const float* resid, float* xout, const float* alpha,
                  void* sout, int s_f32, const int32_t* lens, int in_scale, int out_scale, int nq, int nx, int dx) {
-    auto kern = &k_conv_cl<FM, false, false, NQ>;     // NQ = 8: fp16 output, no residual only
-    if constexpr (NQ == 4)
+    auto kern = &k_conv_cl<FM, false, false, NQ, DA, OCC>;     // NQ = 8: fp16 output, no residual only
+    if constexpr (NQ == 4 && DA == CL_DA)
         kern = resid ? (s_f32 ? &k_conv_cl<FM, true, true, NQ> : &k_conv_cl<FM, false, true, NQ>)
                      : (s_f32 ? &k_conv_cl<FM, true, false, NQ> : kern);
     if (lds > 65536)
@@ -522,18 +537,24 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     // convs, overhead-bound at 128: -6 % / -15 %); the residual convs keep 128 (their prefetched
     // residual tile would not fit the registers beside twice the accumulators), and so do the
     // polyphase ConvTranspose convs (+12-22 % with 256, profiles/r1_dac_wide_tiles_ab.txt)
-    const bool wide = resid == nullptr && !s_f32 && nphase == 1 && FM <= 3 && dac_wide_enabled();
+    // deep (ZK_DAC_DEEP, tuning): the plain k7 convs as one workgroup per CU with 256-position
+    // tiles and CL_DEEP_DA weight slices in flight (the LDS-DMA weight stream is latency-bound at
+    // CL_DA = 3 with two workgroups per CU)
+    const bool deep = resid == nullptr && !s_f32 && nphase == 1 && ks > 1 && dac_deep_enabled();
+    const bool wide = deep || (resid == nullptr && !s_f32 && nphase == 1 && FM <= 3 && dac_wide_enabled());
     const int qt = wide ? 2 * QT : QT;
     const int win = qt + (ks - 1) * dil;
     const size_t xs = (size_t)((win + 15) / 16) * 1024;
     const size_t ws = (size_t)32 * FM * 64;
-    // window lead DX >= CL_DA steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
-    int dx = std::max(CL_DA, ks), nx = 1 + (dx + 1 + ks - 1) / ks;
-    while (dx > CL_DA && CL_NW * ws + nx * xs > 80 * 1024) {
+    const int da = deep ? CL_DEEP_DA : CL_DA;
+    const size_t lds_cap = deep ? 160 * 1024 : 80 * 1024;
+    // window lead DX >= da steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
+    int dx = std::max(da, ks), nx = 1 + (dx + 1 + ks - 1) / ks;
+    while (dx > da && (da + 2) * ws + nx * xs > lds_cap) {
         --dx;
         nx = 1 + (dx + 1 + ks - 1) / ks;
     }
-    const size_t lds = CL_NW * ws + nx * xs;
+    const size_t lds = (da + 2) * ws + nx * xs;
     ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_conv_cl: LDS %zu too large", lds);
     const int nq = (Qn + qt - 1) / qt;
     const long nwg = (long)B * nq * (Cout / (32 * FM)) * nphase;
@@ -543,6 +564,21 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     launch_conv<F_, NQ_>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad, Qn, nphase, \
                          out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32, lens, in_scale, out_scale, nq, \
                          nx, dx)
+#define ZK_CLD(F_)                                                                                                \
+    launch_conv<F_, 8, CL_DEEP_DA, 1>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad,  \
+                                     Qn, nphase, out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32,  \
+                                     lens, in_scale, out_scale, nq, nx, dx)
+    if (deep) {
+        switch (FM) {
+            case 4: ZK_CLD(4); break;
+            case 3: ZK_CLD(3); break;
+            case 2: ZK_CLD(2); break;
+            default: ZK_CLD(1); break;
+        }
+        ZK_CHECK_LAUNCH("zk_dac_conv_cl");
+        return 0;
+    }
+#undef ZK_CLD
     switch (FM) {
         case 4: ZK_CL(4, 4); break;
         case 3: if (wide) ZK_CL(3, 8); else ZK_CL(3, 4); break;
