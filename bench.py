@@ -210,8 +210,8 @@ def mamba_roofline(eng):
         L = eng.layers[eng.mamba_ids[j]]
         return lambda st: call("zk_mamba_step", ptr(ws["part"]), gs, R, c.d_inner, c.nheads_ssm, c.headdim,
                                c.d_state, ptr(L["conv_w"]), ptr(L["conv_b"]), ptr(ws["conv"][j][0]),
-                               ptr(ws["conv"][j][1]), ptr(ws["scal"][1:2]), ptr(ws["ssm"][j]), ptr(L["A"]),
-                               ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), None, st)
+                               ptr(ws["conv"][j][1]), ptr(ws["scal"][1:2]), ptr(ws["ssm"][j][0]), ptr(ws["ssm"][j][1]),
+                               ptr(L["A"]), ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), None, st)
     per = _time_launches([launch(j) for j in range(len(eng.mamba_ids))], reps=4)
     b = R * c.d_inner * c.d_state * 2 * 2 + R * c.conv_dim * 8 * 2 + gs * R * c.d_in_proj * 4 + R * c.d_inner * 4
     return _roof(b, per, traffic=_pmc_traffic("k_mamba_step", R=R), kernel="k_mamba_step",

@@ -397,17 +397,21 @@ int zk_prefix_cond(const ZkCondPlan* plan, int B, void* out, void* stream);
  * in_proj output columns [z (d_inner) | xBC (conv_dim = d_inner + 2 d_state) | dt (nheads)].
  * Conv state bf16 [R][conv_dim][4] (last 4 inputs), double-buffered by step parity: the step at
  * position *pos_dev reads buffer (pos & 1) of {a, b} and writes the other. SSM state bf16
- * [R][nheads][headdim][d_state]. A = -exp(A_log), dt_bias, D fp32 [nheads]; conv_w fp32
+ * [R][nheads][headdim][d_state]: updated in place when ssm_state_b is NULL, otherwise
+ * double-buffered like the conv state ({ssm_state, ssm_state_b}: read (pos & 1), write the other;
+ * the in-place read-modify-write of the same lines streams ~5 % slower). A = -exp(A_log), dt_bias, D fp32 [nheads]; conv_w fp32
  * [conv_dim][4], conv_b fp32 [conv_dim]. yz (fp32 [rows][d_inner]) = bf16(C.h + D x) * silu(z),
  * normalised by zk_gated_rmsnorm (RMSNormGated, norm_before_gate=False) into the out_proj input.
  * (headdim, d_state) in {(64,128), (64,64), (32,64)}. */
 int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
                   int d_state, const float* conv_w, const float* conv_b, void* conv_state_a,
-                  void* conv_state_b, const int32_t* pos_dev, void* ssm_state, const float* A,
-                  const float* dt_bias, const float* D, float* yz, const int32_t* skip, void* stream);
+                  void* conv_state_b, const int32_t* pos_dev, void* ssm_state, void* ssm_state_b,
+                  const float* A, const float* dt_bias, const float* D, float* yz, const int32_t* skip,
+                  void* stream);
 /* prefill over S positions per row: zx = in_proj output fp32 [R*S][cols] (split 1); xc_scratch
  * bf16 [R*S][conv_dim]; conv_state receives the last 4 inputs (the buffer the first decode step
- * reads); ssm_state receives the final state (bf16). */
+ * reads); ssm_state receives the final state (bf16; with double-buffered decode states, the
+ * buffer the first decode step reads). */
 int zk_mamba_prefill(const float* zx, int R, int S, int d_inner, int nheads, int headdim, int d_state,
                      const float* conv_w, const float* conv_b, void* xc_scratch, void* conv_state,
                      void* ssm_state, const float* A, const float* dt_bias, const float* D, float* yz,

@@ -61,7 +61,8 @@ def test_mamba_step_kernel_vs_oracle(c):
     ssm = ssm0.to(DEV)
     yz = torch.empty(R, c.d_inner, device=DEV)
     call("zk_mamba_step", ptr(parts.to(DEV).contiguous()), gs, R, c.d_inner, c.nheads_ssm, c.headdim, c.d_state,
-         ptr(cw), ptr(cb), ptr(cs_a), ptr(cs_b), ptr(pos), ptr(ssm), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
+         ptr(cw), ptr(cb), ptr(cs_a), ptr(cs_b), ptr(pos), ptr(ssm), None, ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None,
+         s)
     ym = torch.empty(R, c.d_inner, dtype=torch.bfloat16, device=DEV)
     nw = W[p + "norm.weight"].float().to(DEV)
     call("zk_gated_rmsnorm", ptr(yz), R, c.d_inner, ptr(nw), 1e-5, ptr(ym), None, s)
@@ -118,7 +119,8 @@ def test_hybrid_generate_teacher_forced_logits():
 @pytest.mark.parametrize("hp,ds,nh,R,gs,pos", [(32, 64, 16, 6, 2, 5), (64, 128, 64, 8, 2, 6), (64, 128, 64, 3, 1, 7),
                                                (64, 64, 16, 4, 4, 2)])
 def test_mamba_step_grouped_equals_per_head(hp, ds, nh, R, gs, pos, monkeypatch):
-    """The grouped decode kernel (heads per workgroup, B/C conv once per group, pipelined state
+    """Double-buffered SSM state (read buffer pos & 1, write the other) == in place, bit for bit, in
+    both kernels. The grouped decode kernel (heads per workgroup, B/C conv once per group, pipelined state
     slices, whole-line state access at d_state 128) == the per-head kernel: SSM and conv states
     bit for bit; the gated outputs bit for bit, or -- where the row sum y = C.h is reduced in a
     different order (d_state 128: 16 lanes x 8 instead of 4 threads x 32) -- within 1 bf16 ulp of y."""
@@ -138,15 +140,27 @@ def test_mamba_step_grouped_equals_per_head(hp, ds, nh, R, gs, pos, monkeypatch)
     posd = torch.tensor([pos], dtype=torch.int32, device=DEV)
     s = stream_ptr()
     outs = []
-    for grouped in ("0", "1"):
+    for grouped, pingpong in (("0", False), ("1", False), ("1", True), ("0", True)):
         monkeypatch.setenv("ZK_MAMBA_GROUPED", grouped)
         ca, cbuf = conv0.to(DEV), conv0.to(DEV)
         ssm = ssm0.to(DEV)
         yz = torch.full((R, di), float("nan"), device=DEV)
-        call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
-             ptr(ssm), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
-        torch.cuda.synchronize()
+        if pingpong:       # {a, b}: the step at position pos reads (pos & 1) and writes the other
+            other = torch.full_like(ssm, float("nan"))
+            sa, sb = (other, ssm) if pos & 1 else (ssm, other)
+            call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
+                 ptr(sa), ptr(sb), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
+            torch.cuda.synchronize()
+            assert torch.equal(ssm.cpu(), ssm0), "ping-pong read buffer modified"
+            ssm = other
+        else:
+            call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
+                 ptr(ssm), None, ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
+            torch.cuda.synchronize()
         outs.append((ca.cpu(), cbuf.cpu(), ssm.cpu(), yz.cpu()))
+    for i, j in ((1, 2), (0, 3)):       # ping-pong == in place, bit for bit, in each kernel
+        for a, b in zip(outs[i], outs[j]):
+            assert torch.equal(a, b)
     for a, b, name in zip(outs[0][:3], outs[1][:3], ("conv_a", "conv_b", "ssm")):
         assert torch.equal(a, b), name
     ya, yb = outs[0][3], outs[1][3]

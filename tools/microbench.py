@@ -193,7 +193,8 @@ def mamba():
     cb = torch.randn(conv_dim, device=dev) * 0.1
     convs = [(torch.randn(R, conv_dim, 4, device=dev).to(torch.bfloat16),
               torch.randn(R, conv_dim, 4, device=dev).to(torch.bfloat16)) for _ in range(nl)]
-    ssms = [(0.5 * torch.randn(R, nh, hp, ds, device=dev)).to(torch.bfloat16) for _ in range(nl)]
+    # double-buffered state (as the engine runs it)
+    ssms = [(0.5 * torch.randn(2, R, nh, hp, ds, device=dev)).to(torch.bfloat16) for _ in range(nl)]
     A = -torch.rand(nh, device=dev) * 4
     dtb = torch.randn(nh, device=dev) * 0.5
     Dv = torch.randn(nh, device=dev)
@@ -205,7 +206,7 @@ def mamba():
         i = it[0] % nl
         it[0] += 1
         call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(convs[i][0]), ptr(convs[i][1]),
-             ptr(posd), ptr(ssms[i]), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, S)
+             ptr(posd), ptr(ssms[i][0]), ptr(ssms[i][1]), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, S)
     us = timeit(f, reps=40, warm=8)
     b = R * di * ds * 2 * 2 + R * conv_dim * 8 * 2 + gs * R * ncol * 4 + R * di * 4
     print(f"mamba_step R={R} grouped={os.environ.get('ZK_MAMBA_GROUPED', '1')}: {us:7.2f} us  "

@@ -42,6 +42,6 @@ else:
     yz = torch.empty(R * di, device=dev)
     for i in range(12):
         call("zk_mamba_step", ptr(part), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(c0), ptr(c1), ptr(pos),
-             ptr(ssms[i % 3]), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
+             ptr(ssms[i % 3]), None, ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
     print("mamba_step R=128: algorithmic bytes/launch", R * di * ds * 2 * 2 + R * cdim * 8 * 2 + gs * R * nin * 4 + R * di * 4)
 torch.cuda.synchronize()

@@ -49,7 +49,8 @@ template <int HP, int DS>
 __global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
     const float* __restrict__ part, int gs, int R, int di, int nh, const float* __restrict__ conv_w,
     const float* __restrict__ conv_b, const bf16_t* __restrict__ cs_a, bf16_t* __restrict__ cs_b,
-    const int32_t* __restrict__ pos_dev, bf16_t* __restrict__ ssm, const float* __restrict__ A,
+    const int32_t* __restrict__ pos_dev, bf16_t* __restrict__ ssm, bf16_t* __restrict__ ssm_b,
+    const float* __restrict__ A,
     const float* __restrict__ dt_bias, const float* __restrict__ Dv, float* __restrict__ yz,
     const int32_t* __restrict__ skip) {
     constexpr int TPP = MB_THREADS / HP;     // threads per headdim row
@@ -66,9 +67,14 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
     const int par = pos_dev ? (*pos_dev & 1) : 0;
     const bf16_t* csi = (par ? cs_b : cs_a) + (size_t)r * conv_dim * 4;
     bf16_t* cso = (par ? const_cast<bf16_t*>(cs_a) : cs_b) + (size_t)r * conv_dim * 4;
+    // SSM state: in place (ssm_b == nullptr) or ping-pong like the conv state (read buffer pos & 1)
+    const bf16_t* ssr = (ssm_b && par) ? ssm_b : ssm;
+    bf16_t* ssw = ssm_b ? (par ? ssm : ssm_b) : ssm;
     // (loading the state slice before this prologue measured 1 % slower: occupancy 8 -> 7 waves)
     const int t = threadIdx.x, p = t / TPP, n0 = (t % TPP) * EPT;
-    bf16_t* sp = ssm + (((size_t)r * nh + h) * HP + p) * DS + n0;
+    const size_t soff = (((size_t)r * nh + h) * HP + p) * DS + n0;
+    const bf16_t* sp = ssr + soff;
+    bf16_t* spw = ssw + soff;
     uint4 st8[EPT / 8];
 
     for (int i = threadIdx.x; i < HP + 2 * DS + HP + 1; i += MB_THREADS) {
@@ -119,7 +125,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
             sv[e] = s;
             acc += s * s_C[n];
         }
-        *reinterpret_cast<uint4*>(sp + e8) = pack8(sv);
+        *reinterpret_cast<uint4*>(spw + e8) = pack8(sv);
     }
 #pragma unroll
     for (int off = 1; off < TPP; off <<= 1) acc += __shfl_xor(acc, off, 64);
@@ -147,7 +153,8 @@ template <int HP, int DS, int HG, int GS>
 __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
     const float* __restrict__ part, int R, int di, int nh, const float* __restrict__ conv_w,
     const float* __restrict__ conv_b, const bf16_t* __restrict__ cs_a, bf16_t* __restrict__ cs_b,
-    const int32_t* __restrict__ pos_dev, bf16_t* __restrict__ ssm, const float* __restrict__ A,
+    const int32_t* __restrict__ pos_dev, bf16_t* __restrict__ ssm, bf16_t* __restrict__ ssm_b,
+    const float* __restrict__ A,
     const float* __restrict__ dt_bias, const float* __restrict__ Dv, float* __restrict__ yz,
     const int32_t* __restrict__ skip) {
     constexpr int TPP = MB_THREADS / HP;     // threads per headdim row
@@ -167,6 +174,8 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
     const int par = pos_dev ? (*pos_dev & 1) : 0;
     const bf16_t* csi = (par ? cs_b : cs_a) + (size_t)r * conv_dim * 4;
     bf16_t* cso = (par ? const_cast<bf16_t*>(cs_a) : cs_b) + (size_t)r * conv_dim * 4;
+    const bf16_t* ssr = (ssm_b && par) ? ssm_b : ssm;       // SSM state ping-pong (see k_mamba_step)
+    bf16_t* ssw = ssm_b ? (par ? ssm : ssm_b) : ssm;
     const int t = threadIdx.x, p = t / TPP, n0 = (t % TPP) * EPT;
 
     // ---- prologue loads (all issued before any is used)
@@ -205,7 +214,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
         else return (size_t)p * DS + n0 + 8 * v;
     };
     auto load_state = [&](int hh, int buf) {
-        const bf16_t* sb = ssm + ((size_t)r * nh + h0 + hh) * HP * DS;
+        const bf16_t* sb = ssr + ((size_t)r * nh + h0 + hh) * HP * DS;
 #pragma unroll
         for (int v = 0; v < NV; ++v) st[buf][v] = *reinterpret_cast<const uint4*>(sb + st_off(v));
     };
@@ -254,7 +263,6 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
         const float dt = softplus_thr(s_dt[hh] + dt_bias[h]);
         const float dA = expf(dt * A[h]);
         if constexpr (COAL) {
-            bf16_t* sb = ssm + ((size_t)r * nh + h) * HP * DS;
             const int nb = 8 * (ll & 15);
             float Bv[8], Cv[8];
 #pragma unroll
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
                     a += sn * Cv[e];
                 }
                 accv[v] = a;
-                *reinterpret_cast<uint4*>(sb + st_off(v)) = pack8(svv);
+                *reinterpret_cast<uint4*>(ssw + ((size_t)r * nh + h) * HP * DS + st_off(v)) = pack8(svv);
             }
             if (hh + PD < HG) load_state(hh + PD, buf);
 #pragma unroll
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
             continue;
         }
         const float xp = s_x[hh * HP + p];
-        bf16_t* sp = ssm + (((size_t)r * nh + h) * HP + p) * DS + n0;
+        bf16_t* sp = ssw + (((size_t)r * nh + h) * HP + p) * DS + n0;
         float acc = 0.f;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -447,8 +455,9 @@ __global__ __launch_bounds__(MB_THREADS) void k_gated_norm(const float* __restri
 
 extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
                              int d_state, const float* conv_w, const float* conv_b, void* conv_state_a,
-                             void* conv_state_b, const int32_t* pos_dev, void* ssm_state, const float* A,
-                             const float* dt_bias, const float* D, float* yz, const int32_t* skip, void* stream) {
+                             void* conv_state_b, const int32_t* pos_dev, void* ssm_state, void* ssm_state_b,
+                             const float* A, const float* dt_bias, const float* D, float* yz, const int32_t* skip,
+                             void* stream) {
     const int hp = headdim, ds = d_state;
     ZK_REQUIRE(gemm_nsplit >= 1 && gemm_nsplit <= MB_MAXGS, "zk_mamba_step: gemm_nsplit=%d", gemm_nsplit);
     ZK_REQUIRE(nheads * headdim == d_inner, "zk_mamba_step: nheads*headdim != d_inner");
@@ -463,15 +472,15 @@ extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_in
         if (gemm_nsplit == 1)                                                                                      \
             hipLaunchKernelGGL((k_mamba_step_g<HP_, DS_, ZK_MB_HG, 1>), g_, dim3(MB_THREADS), 0, (hipStream_t)stream,     \
                                part, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,             \
-                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip);      \
+                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, (bf16_t*)ssm_state_b, A, dt_bias, D, yz, skip);      \
         else if (gemm_nsplit == 2)                                                                                 \
             hipLaunchKernelGGL((k_mamba_step_g<HP_, DS_, ZK_MB_HG, 2>), g_, dim3(MB_THREADS), 0, (hipStream_t)stream,     \
                                part, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,             \
-                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip);      \
+                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, (bf16_t*)ssm_state_b, A, dt_bias, D, yz, skip);      \
         else                                                                                                       \
             hipLaunchKernelGGL((k_mamba_step_g<HP_, DS_, ZK_MB_HG, 4>), g_, dim3(MB_THREADS), 0, (hipStream_t)stream,     \
                                part, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,             \
-                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip);      \
+                               (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, (bf16_t*)ssm_state_b, A, dt_bias, D, yz, skip);      \
     } while (0)
         ZK_MB_DISPATCH(64, 128, ZK_MB_STEPG)
         ZK_MB_DISPATCH(32, 64, ZK_MB_STEPG)
@@ -485,7 +494,7 @@ extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_in
 #define ZK_MB_STEP(HP_, DS_)                                                                                       \
     hipLaunchKernelGGL((k_mamba_step<HP_, DS_>), dim3(nheads, R), dim3(MB_THREADS), 0, (hipStream_t)stream, part,  \
                        gemm_nsplit, R, d_inner, nheads, conv_w, conv_b, (const bf16_t*)conv_state_a,                \
-                       (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, A, dt_bias, D, yz, skip)
+                       (bf16_t*)conv_state_b, pos_dev, (bf16_t*)ssm_state, (bf16_t*)ssm_state_b, A, dt_bias, D, yz, skip)
     ZK_MB_DISPATCH(64, 128, ZK_MB_STEP)
     ZK_MB_DISPATCH(32, 64, ZK_MB_STEP)
     ZK_MB_DISPATCH(64, 64, ZK_MB_STEP)

@@ -19,6 +19,7 @@ Prefill runs the causal conv over the prefix and the exact recurrence (zk_mamba_
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -190,7 +191,8 @@ class HybridDecoder(HipDecoder):
             key=key, R=R, T=T, Ld=Ld, smax=smax, S_pre=S_pre, splits=splits, attn_splits=attn_splits,
             kv=torch.zeros(max(na, 1), 2, R * Hk * smax * hd, dtype=bf, device=dev),
             conv=torch.zeros(max(nm, 1), 2, R * c.conv_dim * 4, dtype=bf, device=dev),
-            ssm=torch.zeros(max(nm, 1), R * c.nheads_ssm * c.headdim * c.d_state, dtype=bf, device=dev),
+            # double-buffered by step parity like the conv state (zk_mamba_step reads one, writes the other)
+            ssm=torch.zeros(max(nm, 1), 2, R * c.nheads_ssm * c.headdim * c.d_state, dtype=bf, device=dev),
             x=torch.empty(Mp, D, dtype=bf, device=dev), xn=torch.empty(Mp, D, dtype=bf, device=dev),
             q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
             h=torch.empty(Mp, max(Fd, 1), dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
@@ -223,6 +225,7 @@ class HybridDecoder(HipDecoder):
         x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
         scal = ws["scal"]
         pos_dev = None if prefill else ptr(scal[1:2])
+        inplace = os.environ.get("ZK_SSM_INPLACE") == "1"
         for i, L in enumerate(self.layers):
             if i + 1 < len(self.layers):
                 nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
@@ -251,16 +254,20 @@ class HybridDecoder(HipDecoder):
             else:
                 j = self.mamba_ids.index(i)
                 conv, ssm = ws["conv"][j], ws["ssm"][j]
+                # SSM state double-buffered by position parity (ZK_SSM_INPLACE=1: A/B knob, in place)
+                sr = 0 if inplace else S & 1
+                ssm_b = None if inplace else ptr(ssm[1])
                 call("zk_gemm_bf16", ptr(xn), D, ptr(L["w_in"]), M, nin, D, sp["inp"], 0, ptr(part), None, skip,
                      stream)
                 if prefill:
                     # the first decode step (position S) reads conv buffer (S & 1)
                     call("zk_mamba_prefill", ptr(part), R, S, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
-                         ptr(L["conv_b"]), ptr(ws["xc"]), ptr(conv[S & 1]), ptr(ssm), ptr(L["A"]), ptr(L["dt_bias"]),
+                         ptr(L["conv_b"]), ptr(ws["xc"]), ptr(conv[S & 1]), ptr(ssm[sr]), ptr(L["A"]),
+                         ptr(L["dt_bias"]),
                          ptr(L["D"]), ptr(ws["yz"]), stream)
                 else:
                     call("zk_mamba_step", ptr(part), sp["inp"], R, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
-                         ptr(L["conv_b"]), ptr(conv[0]), ptr(conv[1]), pos_dev, ptr(ssm), ptr(L["A"]),
+                         ptr(L["conv_b"]), ptr(conv[0]), ptr(conv[1]), pos_dev, ptr(ssm[0]), ssm_b, ptr(L["A"]),
                          ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), skip, stream)
                 call("zk_gated_rmsnorm", ptr(ws["yz"]), M, di, ptr(L["norm_w"]), 1e-5, ptr(ws["ym"]), skip, stream)
                 call("zk_gemm_bf16", ptr(ws["ym"]), di, ptr(L["w_out"]), M, D, di, sp["out"], 0, ptr(part), None,
