@@ -602,8 +602,13 @@ constexpr int GF_XS = 2048 + 8;    // LDS row stride (bf16) of the LayerNorm'd r
 // and the prologue merges them exactly as k_attn_combine does (backbone.hip) into LDS; each
 // wave merges the 2 heads of its own K range (K = 2048, NW = 8), rows < M <= 2.
 constexpr int GF_AT_G = 4, GF_AT_STR = 2 * GF_AT_G + GF_AT_G * 128;    // = AT_G, AT_STR (attn_common.h)
-template <int MODE, bool LN, int NTW, bool HALF, int NW, int KS, int PF, int MRG = 0>
-__global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict__ A, long lda,
+// XR: rows the LDS activation image holds (2 for B = 1, 16 otherwise): a 16-row image is 66 KB and
+// caps the LayerNorm-prologue GEMVs at 2 workgroups per CU; the 2-row image (8 KB) does not.
+#ifndef ZK_GF_OCC2
+#define ZK_GF_OCC2 1               // min waves per SIMD the B = 1 (XR = 2) instantiations are sized for
+#endif
+template <int MODE, bool LN, int NTW, bool HALF, int NW, int KS, int PF, int MRG = 0, int XR = 16>
+__global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(const bf16_t* __restrict__ A, long lda,
                                                        const bf16_t* __restrict__ W, int M, int N, int K,
                                                        const bf16_t* __restrict__ lnw, const bf16_t* __restrict__ lnb,
                                                        float eps, float* __restrict__ Cf, bf16_t* __restrict__ Cb,
@@ -617,8 +622,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemv_f(const bf16_t* __restrict_
     constexpr int KPL = HALF ? 2 : 1;                                // k-steps per weight load
     constexpr int NL = KS / KPL;                                     // weight loads per wave and tile
     static_assert(NL * KPL == KS, "HALF pairs k-steps");
-    constexpr int MR = 16 / NW;                                      // LN rows per wave
-    __shared__ __attribute__((aligned(16))) uint4 xs[XS ? 16 * GF_XS / 8 : 1];
+    constexpr int MR = (XR + NW - 1) / NW;                           // LN rows per wave
+    static_assert(!MRG || XR == 2, "merge prologue: M <= 2");
+    __shared__ __attribute__((aligned(16))) uint4 xs[XS ? XR * GF_XS / 8 : 1];
     __shared__ __attribute__((aligned(16))) f32x4 red[NW][NTW][64];
     if (skip && *skip) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1009,6 +1015,17 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     return 0;
 }
 
+namespace {
+// ZK_GF_XR2=0: 16-row LDS image at B = 1 too (A/B knob, read once)
+bool gf_xr2() {
+    static const bool on = [] {
+        const char* e = getenv("ZK_GF_XR2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+}  // namespace
+
 extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, int mode,
                              const void* ln_w, const void* ln_b, float eps, float* Cf, void* Cb,
                              const int32_t* skip_flag, void* stream) {
@@ -1031,6 +1048,11 @@ extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int 
         return e ? atoi(e) : -1;
     }();
     if (lay_force >= 0 && !(lay_force == 0 && mode == 1)) lay = lay_force;
+    static const bool b1_lay1 = [] {      // B = 1: one tile per workgroup for the wide LN GEMVs (fc1, heads)
+        const char* e = getenv("ZK_GF_B1_LAY1");
+        return e && e[0] == '1';
+    }();
+    if (lay_force < 0 && b1_lay1 && M <= 2 && ln_w && lay == 2) lay = 1;
     const int grid = lay == 0 ? 2 * tiles : (lay == 2 ? (tiles + 1) / 2 : tiles);
     const bool ln = ln_w != nullptr;
     (void)ln;
@@ -1045,14 +1067,24 @@ extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int 
 #ifndef ZK_GF_PF
 #define ZK_GF_PF 8
 #endif
+#ifndef ZK_GF_PF2
+#define ZK_GF_PF2 ZK_GF_PF         // k-steps in flight of the B = 1 (XR = 2) instantiations
+#endif
 #define ZK_GF(MODE_, LN_, NTW_, HALF_, NW_, KSW_)                                                            \
     do {                                                                                                      \
         constexpr int KS_ = (KSW_) / (NW_);                                                                   \
         constexpr int NL_ = HALF_ ? KS_ / 2 : KS_;                                                            \
-        hipLaunchKernelGGL((k_gemv_f<MODE_, LN_, NTW_, HALF_, NW_, KS_, (NL_ < ZK_GF_PF ? NL_ : ZK_GF_PF)>),  \
-                           dim3(grid), dim3(64 * (NW_)), 0, (hipStream_t)stream, (const bf16_t*)A, lda,        \
-                           (const bf16_t*)W, M, N, K, (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, Cf,        \
-                           (bf16_t*)Cb, skip_flag);                                                            \
+        if (M <= 2 && gf_xr2())                                                                               \
+            hipLaunchKernelGGL((k_gemv_f<MODE_, LN_, NTW_, HALF_, NW_, KS_, (NL_ < ZK_GF_PF2 ? NL_ : ZK_GF_PF2),  \
+                                          0, 2>),                                                             \
+                               dim3(grid), dim3(64 * (NW_)), 0, (hipStream_t)stream, (const bf16_t*)A, lda,    \
+                               (const bf16_t*)W, M, N, K, (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, Cf,    \
+                               (bf16_t*)Cb, skip_flag, nullptr, 1);                                            \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_gemv_f<MODE_, LN_, NTW_, HALF_, NW_, KS_, (NL_ < ZK_GF_PF ? NL_ : ZK_GF_PF)>),  \
+                               dim3(grid), dim3(64 * (NW_)), 0, (hipStream_t)stream, (const bf16_t*)A, lda,    \
+                               (const bf16_t*)W, M, N, K, (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, Cf,    \
+                               (bf16_t*)Cb, skip_flag, nullptr, 1);                                            \
         handled = true;                                                                                       \
     } while (0)
 #define ZK_GF_LAY(MODE_, LN_, KSW_)                                     \
@@ -1088,7 +1120,7 @@ extern "C" int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const vo
     ZK_REQUIRE(work != nullptr && x != nullptr, "zk_gemv_attn_out: null buffer");
     const int grid = 2 * ((N + 15) / 16);                   // half tiles, 8 K-range waves
 #define ZK_GAO(NS_)                                                                                              \
-    hipLaunchKernelGGL((k_gemv_f<2, false, 1, true, 8, 8, 4, NS_>), dim3(grid), dim3(512), 0,                  \
+    hipLaunchKernelGGL((k_gemv_f<2, false, 1, true, 8, 8, 4, NS_, 2>), dim3(grid), dim3(512), 0,               \
                        (hipStream_t)stream, reinterpret_cast<const bf16_t*>(work), (long)K, (const bf16_t*)W, M,  \
                        N, K, nullptr, nullptr, 0.f, nullptr, (bf16_t*)x, skip_flag, work, Hkv)
     switch (nsplit) {
