@@ -276,6 +276,54 @@ int zk_sample_heads(const float* part, int nsplit, const zk_gen_state* st, const
  * first frame (model.py:310-319). */
 int zk_eos_step(const zk_gen_state* st, int prefill, int prefix_len, void* stream);
 
+/* ------------------------------------------------------------------ one decode step
+ * The whole autoregressive step of Zonos.generate (model.py:322-424: _decode_one_token's
+ * embed -> 26 blocks -> norm_f -> 9 heads -> CFG, then the sampler, the EOS protocol and the
+ * delayed-frame write) enqueued on `stream` with no host synchronisation, exactly the launch
+ * sequence of zonos_amd.engine.HipDecoder._decode_step (the Python engine calls this entry):
+ * small = 1 (B <= 8): five launches per block (zk_gemv_fused LayerNorm prologues / residual
+ * epilogues; attn_merge > 0: zk_attn_decode_qkv_part + zk_gemv_attn_out); small = 0: seven
+ * (split-K zk_gemm_bf16 + zk_attn_decode_qkv_sc + zk_resid_ln). Every position/offset is read
+ * from st.scal on the device, so one call is captured once into a hipGraph and replayed.
+ * Replaces the per-token Python loop body of model.py:322-424 for a C/C++ host. */
+typedef struct zk_step_layer {
+    const void* ln1_w;    /* norm.weight / bias (bf16 [D]) */
+    const void* ln1_b;
+    const void* wqkv;     /* mixer.in_proj, packed (zk_pack_weights) */
+    const void* wo;       /* mixer.out_proj, packed */
+    const void* ln2_w;    /* norm2 */
+    const void* ln2_b;
+    const void* fc1;      /* mlp.fc1 in zk_permute_fc1 order, packed */
+    const void* fc2;      /* mlp.fc2, packed */
+    void* k_cache;        /* this layer's K / V^T cache (fragment order, Smax keys per (row, kv head)) */
+    void* vt_cache;
+} zk_step_layer;
+
+typedef struct zk_step_desc {
+    int32_t B, n_layer, d_model, n_heads, n_kv, head_dim, d_ff, smax;
+    int32_t split_qkv, split_o, split_fc2, split_heads;   /* split-K counts (small = 0) */
+    int32_t attn_splits, attn_merge, rope_neox, small;
+    float eps;
+    const zk_step_layer* layers;   /* [n_layer] */
+    const void* emb;               /* codebook embeddings bf16 [9][1026][D] */
+    const void* heads;             /* 9 heads stacked, packed */
+    const void* lnf_w;             /* norm_f */
+    const void* lnf_b;
+    const float* freqs;            /* RoPE table (engine.rope_table) */
+    void* x;                       /* residual rows bf16 [2B][D] */
+    void* xn;                      /* LayerNorm'd rows bf16 [2B][D] */
+    void* y;                       /* attention output bf16 [2B][H*hd] */
+    void* h;                       /* SwiGLU output bf16 [2B][d_ff] */
+    float* part;                   /* split-K slabs / logits */
+    float* attn_work;              /* split-KV partials */
+    uint32_t* attn_cnt;            /* in-launch combine tickets [2B][Hkv] */
+    float* dbg;                    /* nullable: fp32 CFG logits of draw 0 */
+    zk_gen_state st;
+    zk_sampling_params sp;
+} zk_step_desc;
+
+int zk_decode_step(const zk_step_desc* d, void* stream);
+
 /* ------------------------------------------------------------------ DAC decoder
  * (zonos/autoencoder.py:44-47 -> modeling_dac.py:610-640). fp32 activations, layout
  * [B][C][T] (channels-first, like torch). Per-row valid lengths (in frames) make a

@@ -134,6 +134,9 @@ def test_ctypes_struct_layouts_match_the_c_abi(lib):
     assert lib.zk_abi_size(10) == _lib.SmallArgs.prof.offset
     assert lib.zk_abi_size(11) == _lib.SmallArgs.eps.offset
     assert lib.zk_abi_size(12) == _lib.GenState.seed.offset
+    assert lib.zk_abi_size(6) == C.sizeof(_lib.StepLayer) and lib.zk_abi_size(7) == C.sizeof(_lib.StepDesc)
+    assert lib.zk_abi_size(13) == _lib.StepDesc.eps.offset
+    assert lib.zk_abi_size(14) == _lib.StepDesc.st.offset and lib.zk_abi_size(15) == _lib.StepDesc.sp.offset
 
 
 def test_persistent_step_selection():

@@ -206,3 +206,32 @@ def test_force_full_length_and_batch_shard_invariance():
         cb = torch.cat([cond[b:b + 1], cond[B + b:B + b + 1]])
         one = eng.generate(cb, prefix[b:b + 1], 16, 2.0, 1, c["sp"], seed=11, row_base=b, force_full_length=True)
         assert torch.equal(one[0], full[b]), b
+
+
+@pytest.mark.parametrize("geom,B", [("tiny", 1), ("tiny", 12), ("full", 1), ("full", 3), ("full", 12)])
+def test_c_decode_step_equals_python_sequence(geom, B, monkeypatch):
+    """zk_decode_step (the decode step enqueued by the C ABI) == the same launch sequence issued
+    from Python (HipDecoder._decode_step with c_step off): identical codes and per-step logits, on
+    the split-K path (TINY; full width B = 12) and the full-width small-batch path (B = 1: attention
+    key splits merged by out_proj; B = 3: in-launch combine / unsplit)."""
+    from zonos_amd.engine import EngineConfig, HipDecoder
+    from .golden_util import FULL, full_weights
+    c = load_gen_case("greedy")
+    if geom == "tiny":
+        cfg, W = TINY, c["W"]
+    else:
+        cfg, W = FULL, full_weights("random")
+    eng = HipDecoder(EngineConfig(cfg.d_model, cfg.n_layer, cfg.n_heads, cfg.n_kv, cfg.d_ff), W, "cuda")
+    g = torch.Generator().manual_seed(B)
+    cond = (torch.randn(2 * B, 12, cfg.d_model, generator=g) * 0.5).to(torch.bfloat16).cuda()
+    sp = dict(c["sp"])
+    outs = []
+    for flag in (True, False):
+        monkeypatch.setattr(HipDecoder, "c_step", flag)
+        eng._ws = None
+        trace = {}
+        out = eng.generate(cond, None, 20, 2.0, B, sp, seed=5, trace=trace)
+        outs.append(([o.cpu() for o in out], [t.cpu() for t in trace["logits"]]))
+    (ca, la), (cb, lb) = outs
+    assert all(torch.equal(x, y) for x, y in zip(ca, cb))
+    assert len(la) == len(lb) and all(torch.equal(x, y) for x, y in zip(la, lb))

@@ -47,6 +47,20 @@ class SmallArgs(C.Structure):
                 ("p_heads", P), ("sync", P), ("skip", P), ("attn_splits", C.c_int32), ("attn_work", P), ("prof", P)]
 
 
+class StepLayer(C.Structure):
+    _fields_ = [("ln1_w", P), ("ln1_b", P), ("wqkv", P), ("wo", P), ("ln2_w", P), ("ln2_b", P), ("fc1", P),
+                ("fc2", P), ("k_cache", P), ("vt_cache", P)]
+
+
+class StepDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("B", "n_layer", "d_model", "n_heads", "n_kv", "head_dim", "d_ff", "smax",
+                                         "split_qkv", "split_o", "split_fc2", "split_heads", "attn_splits",
+                                         "attn_merge", "rope_neox", "small")] + \
+              [("eps", F), ("layers", P), ("emb", P), ("heads", P), ("lnf_w", P), ("lnf_b", P), ("freqs", P),
+               ("x", P), ("xn", P), ("y", P), ("h", P), ("part", P), ("attn_work", P), ("attn_cnt", P), ("dbg", P),
+               ("st", GenState), ("sp", SamplingParams)]
+
+
 # name -> argtypes (all return int status)
 _SIGS = {
     "zk_version": [],
@@ -69,6 +83,7 @@ _SIGS = {
     "zk_attn_decode_qkv_sc": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, P, P, I, P, P],
     "zk_attn_decode_qkv_part": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, I, P, P],
     "zk_gemv_attn_out": [P, I, I, P, I, I, I, P, P, P],
+    "zk_decode_step": [C.POINTER(StepDesc), P],
     "zk_mamba_step": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "zk_mamba_prefill": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "zk_gated_rmsnorm": [P, I, I, P, F, P, P, P],

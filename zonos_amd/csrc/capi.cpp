@@ -36,6 +36,11 @@ extern "C" long zk_abi_size(int which) {
         case 10: return (long)offsetof(zk_small_args, prof);
         case 11: return (long)offsetof(zk_small_args, eps);
         case 12: return (long)offsetof(zk_gen_state, seed);
+        case 6: return (long)sizeof(zk_step_layer);
+        case 7: return (long)sizeof(zk_step_desc);
+        case 13: return (long)offsetof(zk_step_desc, eps);
+        case 14: return (long)offsetof(zk_step_desc, st);
+        case 15: return (long)offsetof(zk_step_desc, sp);
         default: return -1;
     }
 }
@@ -105,3 +110,78 @@ extern "C" int zk_event_destroy(void* ev) {
     if (ev) HIPCHK(hipEventDestroy((hipEvent_t)ev), "zk_event_destroy");
     return 0;
 }
+
+// ------------------------------------------------------------------ one decode step
+// The launch sequence of zonos_amd.engine.HipDecoder._decode_step (see zonos_hip.h). Each
+// entry below checks its own arguments; the first failing one aborts the step with its message.
+#define ZK_STEP(call)                  \
+    do {                               \
+        if ((call) != 0) return -1;    \
+    } while (0)
+
+extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
+    if (d == nullptr || d->layers == nullptr || d->n_layer <= 0 || d->B <= 0) {
+        zk_set_error("zk_decode_step: bad descriptor");
+        return -1;
+    }
+    const int K = d->st.K, V = d->st.V, B = d->B, R = 2 * B;
+    const int D = d->d_model, H = d->n_heads, Hk = d->n_kv, hd = d->head_dim, Fd = d->d_ff;
+    const int Nqkv = (H + 2 * Hk) * hd;
+    int32_t* scal = d->st.scal;
+    const int32_t* skip = scal + 3;
+    const int32_t* pos = scal + 1;
+    const zk_step_layer& L0 = d->layers[0];
+    // embed_codes (model.py:97-98) + CFG row duplication; layer 0's LayerNorm here unless the
+    // small path runs it in the in_proj prologue
+    ZK_STEP(zk_embed_codes(d->st.delayed, B, 1, K, (long)d->st.Ld * K, d->st.Ld, scal, -1, d->emb, V, D, 2, d->x, 1,
+                           0, d->small ? nullptr : L0.ln1_w, d->small ? nullptr : L0.ln1_b, d->eps,
+                           d->small ? nullptr : d->xn, skip, stream));
+    for (int i = 0; i < d->n_layer; ++i) {
+        const zk_step_layer& L = d->layers[i];
+        if (d->small) {
+            ZK_STEP(zk_gemv_fused(d->x, D, L.wqkv, R, Nqkv, D, 0, L.ln1_w, L.ln1_b, d->eps, d->part, nullptr, skip,
+                                  stream));
+            if (d->attn_merge > 0) {
+                ZK_STEP(zk_attn_decode_qkv_part(d->part, 1, d->freqs, L.k_cache, L.vt_cache, R, H, Hk, hd, d->smax, 1,
+                                                pos, d->attn_work, d->attn_merge, d->rope_neox, skip, stream));
+                ZK_STEP(zk_gemv_attn_out(d->attn_work, d->attn_merge, Hk, L.wo, R, D, H * hd, d->x, skip, stream));
+            } else {
+                ZK_STEP(zk_attn_decode_qkv_sc(d->part, 1, d->freqs, L.k_cache, L.vt_cache, R, H, Hk, hd, d->smax, 1,
+                                              pos, d->attn_work, d->attn_splits, d->attn_cnt, d->y, d->rope_neox,
+                                              skip, stream));
+                ZK_STEP(zk_gemv_fused(d->y, H * hd, L.wo, R, D, H * hd, 2, nullptr, nullptr, d->eps, nullptr, d->x,
+                                      skip, stream));
+            }
+            ZK_STEP(zk_gemv_fused(d->x, D, L.fc1, R, 2 * Fd, D, 1, L.ln2_w, L.ln2_b, d->eps, nullptr, d->h, skip,
+                                  stream));
+            ZK_STEP(zk_gemv_fused(d->h, Fd, L.fc2, R, D, Fd, 2, nullptr, nullptr, d->eps, nullptr, d->x, skip,
+                                  stream));
+        } else {
+            ZK_STEP(zk_gemm_bf16(d->xn, D, L.wqkv, R, Nqkv, D, d->split_qkv, 0, d->part, nullptr, skip, stream));
+            ZK_STEP(zk_attn_decode_qkv_sc(d->part, d->split_qkv, d->freqs, L.k_cache, L.vt_cache, R, H, Hk, hd,
+                                          d->smax, 1, pos, d->attn_work, d->attn_splits, d->attn_cnt, d->y,
+                                          d->rope_neox, skip, stream));
+            ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, R, D, H * hd, d->split_o, 0, d->part, nullptr, skip, stream));
+            ZK_STEP(zk_resid_ln(d->part, d->split_o, d->x, L.ln2_w, L.ln2_b, d->eps, R, D, d->x, d->xn, 0, skip,
+                                stream));
+            ZK_STEP(zk_gemm_bf16(d->xn, D, L.fc1, R, 2 * Fd, D, 1, 1, nullptr, d->h, skip, stream));
+            ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, R, D, Fd, d->split_fc2, 0, d->part, nullptr, skip, stream));
+            const bool last = i + 1 == d->n_layer;
+            ZK_STEP(zk_resid_ln(d->part, d->split_fc2, d->x, last ? d->lnf_w : d->layers[i + 1].ln1_w,
+                                last ? d->lnf_b : d->layers[i + 1].ln1_b, d->eps, R, D, d->x, d->xn, 0, skip,
+                                stream));
+        }
+    }
+    // 9 heads (model.py:104-111): small path with norm_f as the GEMV prologue, one slab
+    if (d->small)
+        ZK_STEP(zk_gemv_fused(d->x, D, d->heads, R, K * V, D, 0, d->lnf_w, d->lnf_b, d->eps, d->part, nullptr, skip,
+                              stream));
+    else
+        ZK_STEP(zk_gemm_bf16(d->xn, D, d->heads, R, K * V, D, d->split_heads, 0, d->part, nullptr, skip, stream));
+    const int nsp = d->small ? 1 : d->split_heads;
+    ZK_STEP(zk_sample_heads(d->part, nsp, &d->st, &d->sp, 0, 0, d->dbg, stream));
+    ZK_STEP(zk_sample_heads(d->part, nsp, &d->st, &d->sp, 0, 1, nullptr, stream));
+    ZK_STEP(zk_eos_step(&d->st, 0, 0, stream));
+    return 0;
+}
+#undef ZK_STEP

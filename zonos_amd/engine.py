@@ -397,9 +397,34 @@ class HipDecoder(HipBackbone):
                         ptr(ws["stopping"]), ptr(ws["act"]), ptr(ws["rp"]), ptr(ws["tok0"]), ptr(ws["tok1"]),
                         ptr(ws["delayed"]), B, N_CB, ws["Ld"], VOCAB, seed & 0xFFFFFFFFFFFFFFFF, row_base)
 
+    # the step's launch sequence is enqueued by the C ABI (zk_decode_step); ZK_C_STEP=0 runs the
+    # same sequence from Python (bit-identical; kept as the reference for the test)
+    c_step = os.environ.get("ZK_C_STEP", "1") != "0"
+
+    def _step_desc(self, ws, B, st, sp):
+        """zk_step_desc of this workspace: per-layer weights + KV caches, buffers, state, params."""
+        c = self.cfg
+        if "step_layers" not in ws:
+            arr = (_lib.StepLayer * c.n_layer)()
+            for i, L in enumerate(self.layers):
+                kc, vt = self._kv(ws, i)
+                arr[i] = _lib.StepLayer(ptr(L["ln1_w"]), ptr(L["ln1_b"]), ptr(L["wqkv"]), ptr(L["wo"]),
+                                        ptr(L["ln2_w"]), ptr(L["ln2_b"]), ptr(L["fc1"]), ptr(L["fc2"]), ptr(kc), ptr(vt))
+            ws["step_layers"] = arr
+        sps = ws["splits"]
+        return _lib.StepDesc(B, c.n_layer, c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff, ws["smax"],
+                             sps["qkv"], sps["o"], sps["fc2"], sps["heads"], ws["attn_splits"],
+                             ws.get("attn_merge", 0), self.rope_neox, int(self._small(2 * B)), c.eps,
+                             C.cast(ws["step_layers"], C.c_void_p), ptr(self.emb), ptr(self.heads), ptr(self.lnf_w),
+                             ptr(self.lnf_b), ptr(self.freqs), ptr(ws["x"]), ptr(ws["xn"]), ptr(ws["y"]), ptr(ws["h"]),
+                             ptr(ws["part"]), ptr(ws["attn_work"]), ptr(ws["attn_cnt"]), ptr(ws["dbg"]), st, sp)
+
     def _decode_step(self, ws, B, st, sp, stream):
         c = self.cfg
         R = 2 * B
+        if self.c_step and "small" not in ws:
+            call("zk_decode_step", C.byref(self._step_desc(ws, B, st, sp)), stream)
+            return
         scal = ws["scal"]
         skip = ptr(scal[3:4])
         L0 = self.layers[0]

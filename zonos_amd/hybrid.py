@@ -97,6 +97,7 @@ class HybridDecoder(HipDecoder):
     """generate() for the hybrid backbone (the layer loop and state differ from HipDecoder)."""
 
     small_batch_path = False      # the hybrid block sequence has its own _layers (prenorm add + norm)
+    c_step = False                # zk_decode_step is the transformer's sequence; the hybrid's stays here
 
     def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda"):
         _lib.load()
