@@ -324,6 +324,15 @@ typedef struct zk_step_desc {
 
 int zk_decode_step(const zk_step_desc* d, void* stream);
 
+/* The prefill of Zonos.generate (model.py:297-319, _prefill 181-202) on the same descriptor:
+ * x rows [2B][S][D] = [prefix conditioning (cond, bf16 [2B][Lc][D]) | codebook embeddings of the
+ * P audio-prefix frames + the first delayed frame], layer 0's LayerNorm, the 26 blocks over all
+ * 2B*S positions (split-K 1, causal prefill attention filling the KV cache), the heads on the
+ * last position, the first sample (model.py:304: no bias, no penalty) and the first frame write.
+ * S = Lc + P + 1; q: bf16 [2B*S][H*hd] scratch; x / xn / y / h / part sized for 2B*S rows.
+ * The loop state (st.scal, eos_mode, ...) is initialised by the host afterwards (model.py:316-342). */
+int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P, void* q, void* stream);
+
 /* ------------------------------------------------------------------ DAC decoder
  * (zonos/autoencoder.py:44-47 -> modeling_dac.py:610-640). fp32 activations, layout
  * [B][C][T] (channels-first, like torch). Per-row valid lengths (in frames) make a

@@ -210,8 +210,9 @@ def test_force_full_length_and_batch_shard_invariance():
 
 @pytest.mark.parametrize("geom,B", [("tiny", 1), ("tiny", 12), ("full", 1), ("full", 3), ("full", 12)])
 def test_c_decode_step_equals_python_sequence(geom, B, monkeypatch):
-    """zk_decode_step (the decode step enqueued by the C ABI) == the same launch sequence issued
-    from Python (HipDecoder._decode_step with c_step off): identical codes and per-step logits, on
+    """zk_prefill + zk_decode_step (prefill and decode step enqueued by the C ABI) == the same launch
+    sequences issued from Python (HipDecoder with c_step off): identical codes and per-step logits
+    (the first entry is the prefill's), on
     the split-K path (TINY; full width B = 12) and the full-width small-batch path (B = 1: attention
     key splits merged by out_proj; B = 3: in-launch combine / unsplit)."""
     from zonos_amd.engine import EngineConfig, HipDecoder

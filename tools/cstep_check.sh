@@ -4,7 +4,7 @@ set -e
 export TMPDIR=/tmp
 O=gpurun_out/cstep
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_generate.py -k c_decode_step > $O/t1.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_generate.py -k "c_decode_step or full_c1 or dropin" > $O/t1.log 2>&1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > $O/tests.log 2>&1
 : > $O/ab.txt
 for v in 1 0; do

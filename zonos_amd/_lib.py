@@ -84,6 +84,7 @@ _SIGS = {
     "zk_attn_decode_qkv_part": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, I, P, P],
     "zk_gemv_attn_out": [P, I, I, P, I, I, I, P, P, P],
     "zk_decode_step": [C.POINTER(StepDesc), P],
+    "zk_prefill": [C.POINTER(StepDesc), P, I, I, P, P],
     "zk_mamba_step": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "zk_mamba_prefill": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "zk_gated_rmsnorm": [P, I, I, P, F, P, P, P],

@@ -184,4 +184,48 @@ extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
     ZK_STEP(zk_eos_step(&d->st, 0, 0, stream));
     return 0;
 }
+
+extern "C" int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P, void* q, void* stream) {
+    if (d == nullptr || d->layers == nullptr || d->n_layer <= 0 || d->B <= 0 || cond == nullptr || q == nullptr ||
+        Lc < 0 || P < 0) {
+        zk_set_error("zk_prefill: bad arguments");
+        return -1;
+    }
+    const int K = d->st.K, V = d->st.V, B = d->B, R = 2 * B, S = Lc + P + 1, M = R * S;
+    const int D = d->d_model, H = d->n_heads, Hk = d->n_kv, hd = d->head_dim, Fd = d->d_ff;
+    const int Nqkv = (H + 2 * Hk) * hd;
+    const size_t row = (size_t)D * 2;
+    // prefix conditioning into the first Lc positions of every row (model.py:184-186)
+    if (Lc > 0) {
+        hipError_t e = hipMemcpy2DAsync(d->x, S * row, cond, Lc * row, Lc * row, R, hipMemcpyDeviceToDevice,
+                                        (hipStream_t)stream);
+        if (e != hipSuccess) {
+            zk_set_error("zk_prefill: conditioning copy: %s", hipGetErrorString(e));
+            return -1;
+        }
+    }
+    ZK_STEP(zk_embed_codes(d->st.delayed, B, P + 1, K, (long)d->st.Ld * K, d->st.Ld, nullptr, 0, d->emb, V, D, 2,
+                           d->x, S, Lc, nullptr, nullptr, d->eps, nullptr, nullptr, stream));
+    ZK_STEP(zk_layernorm(d->x, d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, M, D, d->xn, stream));
+    for (int i = 0; i < d->n_layer; ++i) {
+        const zk_step_layer& L = d->layers[i];
+        ZK_STEP(zk_gemm_bf16(d->xn, D, L.wqkv, M, Nqkv, D, 1, 0, d->part, nullptr, nullptr, stream));
+        ZK_STEP(zk_qkv_rope(d->part, 1, R, S, H, Hk, hd, d->freqs, 0, nullptr, q, L.k_cache, L.vt_cache, d->smax,
+                            nullptr, d->rope_neox, nullptr, stream));
+        ZK_STEP(zk_attn_prefill(q, L.k_cache, L.vt_cache, R, S, H, Hk, hd, d->smax, d->y, stream));
+        ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, M, D, H * hd, 1, 0, d->part, nullptr, nullptr, stream));
+        ZK_STEP(zk_resid_ln(d->part, 1, d->x, L.ln2_w, L.ln2_b, d->eps, M, D, d->x, d->xn, 0, nullptr, stream));
+        ZK_STEP(zk_gemm_bf16(d->xn, D, L.fc1, M, 2 * Fd, D, 1, 1, nullptr, d->h, nullptr, stream));
+        ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, M, D, Fd, 1, 0, d->part, nullptr, nullptr, stream));
+        const bool last = i + 1 == d->n_layer;
+        ZK_STEP(zk_resid_ln(d->part, 1, d->x, last ? d->lnf_w : d->layers[i + 1].ln1_w,
+                            last ? d->lnf_b : d->layers[i + 1].ln1_b, d->eps, M, D, d->x, d->xn, 0, nullptr, stream));
+    }
+    // heads on the last position of every row (rows r*S + S-1 via lda = S*D)
+    ZK_STEP(zk_gemm_bf16(static_cast<const char*>(d->xn) + (size_t)(S - 1) * row, (long)S * D, d->heads, R, K * V, D,
+                         d->split_heads, 0, d->part, nullptr, nullptr, stream));
+    ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 1, 0, d->dbg, stream));
+    ZK_STEP(zk_eos_step(&d->st, 1, P + 1, stream));
+    return 0;
+}
 #undef ZK_STEP

@@ -493,17 +493,22 @@ class HipDecoder(HipBackbone):
         ws["scal"].zero_()
 
         # ---- prefill (model.py:297-319, _prefill 181-202)
-        x = ws["x"][: R * S].view(R, S, D)
-        x[:, :Lc].copy_(prefix_conditioning.to(torch.bfloat16))
-        call("zk_embed_codes", ptr(ws["delayed"]), B, P + 1, N_CB, Ld * N_CB, Ld, None, 0, ptr(self.emb), VOCAB, D,
-             2, ptr(ws["x"]), S, Lc, None, None, c.eps, None, None, stream)
-        L0 = self.layers[0]
-        call("zk_layernorm", ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, R * S, D, ptr(ws["xn"]), stream)
-        self._layers(ws, R * S, R, S, True, stream, None)
-        self._heads(ws, R, S, stream, None)
-        call("zk_sample_heads", ptr(ws["part"]), ws["splits"]["heads"], C_ref(st), C_ref(sp), 1, 0, ptr(ws["dbg"]),
-             stream)
-        call("zk_eos_step", C_ref(st), 1, P + 1, stream)
+        if self.c_step:        # the same sequence enqueued by the C ABI
+            condb = ws["cond_keep"] = prefix_conditioning.to(torch.bfloat16).contiguous()   # alive until copied
+            call("zk_prefill", C.byref(self._step_desc(ws, B, st, sp)), ptr(condb), Lc, P, ptr(ws["q"]), stream)
+        else:
+            x = ws["x"][: R * S].view(R, S, D)
+            x[:, :Lc].copy_(prefix_conditioning.to(torch.bfloat16))
+            call("zk_embed_codes", ptr(ws["delayed"]), B, P + 1, N_CB, Ld * N_CB, Ld, None, 0, ptr(self.emb), VOCAB,
+                 D, 2, ptr(ws["x"]), S, Lc, None, None, c.eps, None, None, stream)
+            L0 = self.layers[0]
+            call("zk_layernorm", ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, R * S, D, ptr(ws["xn"]),
+                 stream)
+            self._layers(ws, R * S, R, S, True, stream, None)
+            self._heads(ws, R, S, stream, None)
+            call("zk_sample_heads", ptr(ws["part"]), ws["splits"]["heads"], C_ref(st), C_ref(sp), 1, 0,
+                 ptr(ws["dbg"]), stream)
+            call("zk_eos_step", C_ref(st), 1, P + 1, stream)
         if _after_prefill is not None:      # test hook (teacher forcing of the first frame)
             _after_prefill(ws["delayed"][..., P + 1:P + 2])
         if trace is not None:
