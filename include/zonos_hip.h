@@ -13,6 +13,7 @@
  */
 #ifndef ZONOS_HIP_H
 #define ZONOS_HIP_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -400,6 +401,45 @@ int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* 
  * (s = fp32 output of the final Snake, zk_dac_conv_cl with s_f32 = 1; modeling_dac.py:437-439). */
 int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias,
                    float* out, const int32_t* lens, int scale, void* stream);
+
+/* The whole channels-last DAC decode (DACAutoencoder.decode, autoencoder.py:44-47 ->
+ * DacModel.decode, modeling_dac.py:610-640) as one call: RVQ lookup -> conv1 -> per block
+ * ConvTranspose1d + 3 residual units (k7 dilated + 1x1 with the residual add) -> Snake -> conv2
+ * -> tanh, the launch sequence of zonos_amd.autoencoder.HipDacDecoder._decode_cl. Weights in the
+ * zk_dac_conv_cl layouts (channels padded to 32; zk_dac_prep_w16). codes int64 [B][ncb][T];
+ * lens int32 [B] frames (nullable = all T); out fp32 [B][1][T * prod(strides)]; workspace of
+ * zk_dac_decode_workspace(d, B, T) bytes (device memory). */
+#define ZK_DAC_MAXB 6
+#define ZK_DAC_MAXR 3
+typedef struct zk_dac_resunit {
+    int32_t dil;
+    const float* a1;       /* Snake alpha before the k7 conv */
+    const uint16_t* w1;    /* k7 conv, fp16 [7][C][C] */
+    const float* b1;
+    const float* a2;       /* Snake alpha before the 1x1 conv */
+    const uint16_t* w2;    /* 1x1 conv, fp16 [1][C][C] */
+    const float* b2;
+} zk_dac_resunit;
+typedef struct zk_dac_block {
+    int32_t stride, cin, cout, nres;
+    const float* alpha;    /* Snake alpha before the ConvTranspose1d */
+    const uint16_t* wt;    /* ConvTranspose1d, fp16 [stride][2][cout][cin] */
+    const float* bt;
+    zk_dac_resunit res[ZK_DAC_MAXR];
+} zk_dac_block;
+typedef struct zk_dac_desc {
+    int32_t nblocks, ncb, codebook_size, hidden, cin0, c0;
+    const float* tables;   /* RVQ codebooks projected to the latent (zk_dac_rvq_decode_cl) */
+    const uint16_t* conv1_w;
+    const float* conv1_b;
+    const float* final_alpha;
+    const float* conv2_w;  /* [C][7] fp32 */
+    const float* conv2_b;
+    zk_dac_block blocks[ZK_DAC_MAXB];
+} zk_dac_desc;
+size_t zk_dac_decode_workspace(const zk_dac_desc* d, int B, int T);
+int zk_dac_decode(const zk_dac_desc* d, const int64_t* codes, int B, int T, const int32_t* lens, void* workspace,
+                  size_t workspace_bytes, float* out, void* stream);
 
 /* ---- DAC encoder (prefix audio -> codes; DACAutoencoder.encode, autoencoder.py:27-28 ->
  * DacModel.encode). Convolutions run on zk_dac_conv_cl (channels-last fp16 operands); a strided

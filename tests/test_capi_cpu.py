@@ -137,6 +137,8 @@ def test_ctypes_struct_layouts_match_the_c_abi(lib):
     assert lib.zk_abi_size(6) == C.sizeof(_lib.StepLayer) and lib.zk_abi_size(7) == C.sizeof(_lib.StepDesc)
     assert lib.zk_abi_size(13) == _lib.StepDesc.eps.offset
     assert lib.zk_abi_size(14) == _lib.StepDesc.st.offset and lib.zk_abi_size(15) == _lib.StepDesc.sp.offset
+    assert lib.zk_abi_size(8) == C.sizeof(_lib.DacDesc) and lib.zk_abi_size(17) == C.sizeof(_lib.DacBlock)
+    assert lib.zk_abi_size(16) == _lib.DacDesc.blocks.offset
 
 
 def test_persistent_step_selection():

@@ -78,3 +78,21 @@ def test_dac_fp16_batch_rows_bit_identical():
     hop = dec.spec.hop_length
     assert torch.equal(both[1, :, :L * hop], alone[0])
     assert torch.count_nonzero(both[1, :, L * hop:]) == 0
+
+
+@pytest.mark.parametrize("name", ["dac_tiny", "dac_44k"])
+def test_c_dac_decode_equals_python_sequence(name, monkeypatch):
+    """zk_dac_decode (the whole channels-last DAC decode enqueued by the C ABI) == the same launch
+    sequence issued from Python (HipDacDecoder._decode_cl with c_dac off): bit-identical waveforms,
+    ragged batch included."""
+    from zonos_amd.autoencoder import HipDacDecoder
+    dec, d, c, W = _dec(name, "fp16")
+    codes = torch.from_numpy(d["codes"].astype(np.int64)).cuda()            # [2, 9, T]
+    codes2 = torch.cat([codes, codes.flip(-1)]).contiguous()                   # 4 rows, ragged below
+    T = codes.shape[2]
+    lens = torch.tensor([T, T - 5, T - 1, T - 7], dtype=torch.int32, device="cuda")
+    outs = []
+    for flag in (True, False):
+        monkeypatch.setattr(HipDacDecoder, "c_dac", flag)
+        outs.append(dec.decode_padded(codes2, lens).cpu())
+    assert outs[0].shape == outs[1].shape and torch.equal(outs[0], outs[1])

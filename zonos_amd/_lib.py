@@ -61,6 +61,24 @@ class StepDesc(C.Structure):
                ("st", GenState), ("sp", SamplingParams)]
 
 
+class DacResUnit(C.Structure):
+    _fields_ = [("dil", C.c_int32), ("a1", P), ("w1", P), ("b1", P), ("a2", P), ("w2", P), ("b2", P)]
+
+
+DAC_MAXB, DAC_MAXR = 6, 3
+
+
+class DacBlock(C.Structure):
+    _fields_ = [("stride", C.c_int32), ("cin", C.c_int32), ("cout", C.c_int32), ("nres", C.c_int32),
+                ("alpha", P), ("wt", P), ("bt", P), ("res", DacResUnit * DAC_MAXR)]
+
+
+class DacDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("nblocks", "ncb", "codebook_size", "hidden", "cin0", "c0")] + \
+              [("tables", P), ("conv1_w", P), ("conv1_b", P), ("final_alpha", P), ("conv2_w", P), ("conv2_b", P),
+               ("blocks", DacBlock * DAC_MAXB)]
+
+
 # name -> argtypes (all return int status)
 _SIGS = {
     "zk_version": [],
@@ -85,6 +103,7 @@ _SIGS = {
     "zk_gemv_attn_out": [P, I, I, P, I, I, I, P, P, P],
     "zk_decode_step": [C.POINTER(StepDesc), P],
     "zk_prefill": [C.POINTER(StepDesc), P, I, I, P, P],
+    "zk_dac_decode": [C.POINTER(DacDesc), P, I, I, P, P, C.c_size_t, P, P],
     "zk_mamba_step": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "zk_mamba_prefill": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "zk_gated_rmsnorm": [P, I, I, P, F, P, P, P],
@@ -144,12 +163,15 @@ def load():
     lib.zk_small_sync_words.argtypes = [I]
     lib.zk_abi_size.restype = C.c_long
     lib.zk_abi_size.argtypes = [I]
+    lib.zk_dac_decode_workspace.restype = C.c_size_t
+    lib.zk_dac_decode_workspace.argtypes = [C.POINTER(DacDesc), I, I]
     _lib = lib
     return lib
 
 
 def exported_symbols() -> list[str]:
-    return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_small_sync_words", "zk_abi_size"]
+    return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_small_sync_words", "zk_abi_size",
+                          "zk_dac_decode_workspace"]
 
 
 def call(name: str, *args):

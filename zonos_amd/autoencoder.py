@@ -10,6 +10,7 @@ its per-utterance decode.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 import os
 
@@ -170,9 +171,48 @@ class HipDacDecoder:
         cl["conv2_w"], cl["conv2_b"] = cw.contiguous(), self.conv2_b.contiguous()
         self.cl = cl
 
+    # the decode's launch sequence is enqueued by the C ABI (zk_dac_decode); ZK_C_DAC=0 issues the
+    # same sequence from Python (bit-identical; the reference for the test)
+    c_dac = os.environ.get("ZK_C_DAC", "1") != "0"
+
+    def _dac_desc(self):
+        if getattr(self, "_desc", None) is None:
+            s, cl = self.spec, self.cl
+            d = _lib.DacDesc()
+            d.nblocks, d.ncb, d.codebook_size = len(cl["blocks"]), s.n_codebooks, s.codebook_size
+            d.hidden, d.cin0, d.c0 = s.hidden_size, cl["cin0"], cl["c0"]
+            d.tables, d.conv1_w, d.conv1_b = ptr(self.tables), ptr(cl["conv1_w"]), ptr(cl["conv1_b"])
+            d.final_alpha, d.conv2_w, d.conv2_b = ptr(cl["final_alpha"]), ptr(cl["conv2_w"]), ptr(cl["conv2_b"])
+            assert len(cl["blocks"]) <= _lib.DAC_MAXB
+            for i, blk in enumerate(cl["blocks"]):
+                b = d.blocks[i]
+                b.stride, b.cin, b.cout, b.nres = blk["stride"], blk["cin"], blk["cout"], len(blk["res"])
+                b.alpha, b.wt, b.bt = ptr(blk["alpha"]), ptr(blk["wt"]), ptr(blk["bt"])
+                assert len(blk["res"]) <= _lib.DAC_MAXR
+                for j, ru in enumerate(blk["res"]):
+                    b.res[j] = _lib.DacResUnit(ru["dil"], ptr(ru["a1"]), ptr(ru["w1"]), ptr(ru["b1"]), ptr(ru["a2"]),
+                                               ptr(ru["w2"]), ptr(ru["b2"]))
+            self._desc = d
+        return self._desc
+
     def _decode_cl(self, codes, lens, stream):
         s, cl, dev = self.spec, self.cl, self.device
         B, K, T = codes.shape
+        if self.c_dac and cl["blocks"]:
+            d = self._dac_desc()
+            d.ncb = K
+            nbytes = _lib.load().zk_dac_decode_workspace(C.byref(d), B, T)
+            if nbytes == 0:
+                raise _lib.ZonosHipError("zk_dac_decode_workspace: bad descriptor")
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            hop = 1
+            for blk in cl["blocks"]:
+                hop *= blk["stride"]
+            out = torch.empty(B, 1, T * hop, device=dev)
+            call("zk_dac_decode", C.byref(d), ptr(codes.contiguous()), B, T, ptr(lens), ptr(ws), nbytes, ptr(out),
+                 stream)
+            self._ws_keep = ws          # freed at the next decode (stream-ordered reuse)
+            return out
         f16 = torch.int16
         z = torch.empty(B, T, cl["cin0"], dtype=f16, device=dev)
         call("zk_dac_rvq_decode_cl", ptr(codes), B, K, T, K * T, ptr(self.tables), s.codebook_size, s.hidden_size,

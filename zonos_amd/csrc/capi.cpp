@@ -5,6 +5,7 @@
 #include <stddef.h>
 #include <stdio.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/zonos_hip.h"
@@ -41,6 +42,9 @@ extern "C" long zk_abi_size(int which) {
         case 13: return (long)offsetof(zk_step_desc, eps);
         case 14: return (long)offsetof(zk_step_desc, st);
         case 15: return (long)offsetof(zk_step_desc, sp);
+        case 8: return (long)sizeof(zk_dac_desc);
+        case 16: return (long)offsetof(zk_dac_desc, blocks);
+        case 17: return (long)sizeof(zk_dac_block);
         default: return -1;
     }
 }
@@ -229,3 +233,107 @@ extern "C" int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P
     return 0;
 }
 #undef ZK_STEP
+
+// ------------------------------------------------------------------ DAC decode (whole)
+namespace {
+struct DacPlan {
+    size_t z, a, b, x, tmp, last, total;
+};
+size_t zk_align(size_t v) { return (v + 255) & ~(size_t)255; }
+bool dac_plan(const zk_dac_desc* d, int B, int T, DacPlan& p) {
+    if (d == nullptr || d->nblocks < 0 || d->nblocks > ZK_DAC_MAXB || B <= 0 || T <= 0) return false;
+    size_t L = (size_t)T, act = (size_t)B * T * d->c0, big = 0, lastc = d->c0;
+    for (int i = 0; i < d->nblocks; ++i) {
+        const zk_dac_block& k = d->blocks[i];
+        if (k.nres < 1 || k.nres > ZK_DAC_MAXR) return false;
+        L *= (size_t)k.stride;
+        const size_t n = (size_t)B * L * k.cout;
+        act = std::max(act, n);
+        big = std::max(big, n);
+        lastc = k.cout;
+    }
+    p.z = 0;
+    p.a = zk_align(p.z + (size_t)B * T * d->cin0 * 2);
+    p.b = zk_align(p.a + act * 2);
+    p.x = zk_align(p.b + act * 2);
+    p.tmp = zk_align(p.x + big * 4);
+    p.last = zk_align(p.tmp + act * 2);
+    p.total = zk_align(p.last + (size_t)B * L * lastc * 4);
+    return true;
+}
+}  // namespace
+
+extern "C" size_t zk_dac_decode_workspace(const zk_dac_desc* d, int B, int T) {
+    DacPlan p;
+    return dac_plan(d, B, T, p) ? p.total : 0;
+}
+
+#define ZK_DSTEP(call)                 \
+    do {                               \
+        if ((call) != 0) return -1;    \
+    } while (0)
+
+extern "C" int zk_dac_decode(const zk_dac_desc* d, const int64_t* codes, int B, int T, const int32_t* lens,
+                             void* workspace, size_t workspace_bytes, float* out, void* stream) {
+    DacPlan p;
+    if (!dac_plan(d, B, T, p) || codes == nullptr || out == nullptr || workspace == nullptr) {
+        zk_set_error("zk_dac_decode: bad arguments");
+        return -1;
+    }
+    if (workspace_bytes < p.total) {
+        zk_set_error("zk_dac_decode: workspace %zu bytes < %zu needed", workspace_bytes, p.total);
+        return -1;
+    }
+    char* ws = static_cast<char*>(workspace);
+    uint16_t* z = reinterpret_cast<uint16_t*>(ws + p.z);
+    uint16_t* bufs[2] = {reinterpret_cast<uint16_t*>(ws + p.a), reinterpret_cast<uint16_t*>(ws + p.b)};
+    float* x = reinterpret_cast<float*>(ws + p.x);
+    uint16_t* tmp = reinterpret_cast<uint16_t*>(ws + p.tmp);
+    float* last_act = reinterpret_cast<float*>(ws + p.last);
+    ZK_DSTEP(zk_dac_rvq_decode_cl(codes, B, d->ncb, T, (long)d->ncb * T, d->tables, d->codebook_size, d->hidden,
+                                  d->cin0, z, lens, stream));
+    const float* a_next = d->nblocks ? d->blocks[0].alpha : d->final_alpha;
+    int cur = 0;
+    ZK_DSTEP(zk_dac_conv_cl(z, B, d->cin0, T, d->conv1_w, 0, d->conv1_b, d->c0, 7, 1, 3, T, 1, 1, 0, T, nullptr,
+                            nullptr, a_next, bufs[cur], 0, lens, 1, 1, stream));
+    int L = T, scale = 1, cch = d->c0;
+    const void* act = bufs[cur];
+    bool act_f32 = false;
+    for (int bi = 0; bi < d->nblocks; ++bi) {
+        const zk_dac_block& k = d->blocks[bi];
+        const int st = k.stride, Lo = L * st;
+        uint16_t* s_new = bufs[cur ^ 1];
+        ZK_DSTEP(zk_dac_conv_cl(static_cast<const uint16_t*>(act), B, k.cin, L, k.wt, 2L * k.cout * k.cin, k.bt,
+                                k.cout, 2, 1, 1, L + 1, st, st, -((st + 1) / 2), Lo, nullptr, x, k.res[0].a1, s_new, 0,
+                                lens, scale, scale * st, stream));
+        cur ^= 1;
+        act = s_new;
+        scale *= st;
+        L = Lo;
+        for (int j = 0; j < k.nres; ++j) {
+            const zk_dac_resunit& ru = k.res[j];
+            const float* an = j + 1 < k.nres ? k.res[j + 1].a1 : (bi + 1 < d->nblocks ? d->blocks[bi + 1].alpha
+                                                                                           : d->final_alpha);
+            ZK_DSTEP(zk_dac_conv_cl(static_cast<const uint16_t*>(act), B, k.cout, L, ru.w1, 0, ru.b1, k.cout, 7,
+                                    ru.dil, 3 * ru.dil, L, 1, 1, 0, L, nullptr, nullptr, ru.a2, tmp, 0, lens, scale,
+                                    scale, stream));
+            const bool last = j + 1 == k.nres && bi + 1 == d->nblocks;
+            void* s_out = last ? static_cast<void*>(last_act) : const_cast<void*>(act);
+            ZK_DSTEP(zk_dac_conv_cl(tmp, B, k.cout, L, ru.w2, 0, ru.b2, k.cout, 1, 1, 0, L, 1, 1, 0, L, x, x, an, s_out,
+                                    last ? 1 : 0, lens, scale, scale, stream));
+            if (last) {
+                act = last_act;
+                act_f32 = true;
+            }
+        }
+        cch = k.cout;
+    }
+    if (!act_f32) {
+        zk_set_error("zk_dac_decode: the tail needs at least one block (fp32 Snake input)");
+        return -1;
+    }
+    ZK_DSTEP(zk_dac_tail_cl(static_cast<const float*>(act), B, cch, L, d->conv2_w, d->conv2_b, out, lens, scale,
+                            stream));
+    return 0;
+}
+#undef ZK_DSTEP
