@@ -297,6 +297,72 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln_d2k(const float* part, int n
 }
 
 
+// 512-thread form of k_resid_ln_d2k (default; ZK_RL512=0 selects the 256-thread form): thread t owns float4 piece t of the row,
+// so each wave issues half the slab loads; LayerNorm sums over 8 waves
+template <int NS>
+__global__ __launch_bounds__(512) void k_resid_ln_d2k512(const float* part, int nsplit, const bf16_t* x_in,
+                                                         const bf16_t* w, const bf16_t* b, float eps, int rows,
+                                                         bf16_t* x_out, bf16_t* xn_out, int ln_on_sum,
+                                                         const int32_t* skip) {
+    constexpr int D = 2048;
+    __shared__ float red[16];
+    if (skip && *skip) return;
+    const int row = blockIdx.x, t = threadIdx.x;
+    const size_t slab = (size_t)rows * D;
+    const int c0 = 4 * t;
+    const uint2 w0 = *reinterpret_cast<const uint2*>(w + c0);
+    const uint2 b0 = *reinterpret_cast<const uint2*>(b + c0);
+    const uint2 x0 = *reinterpret_cast<const uint2*>(x_in + (size_t)row * D + c0);
+    const float* p = part + (size_t)row * D;
+    constexpr int NL = NS ? NS : RL_MAXS;
+    float4 a0[NL];
+#pragma unroll
+    for (int sp = 0; sp < NL; ++sp)
+        a0[sp] = *reinterpret_cast<const float4*>(p + (size_t)(NS ? sp : min(sp, nsplit - 1)) * slab + c0);
+    float acc[4] = {a0[0].x, a0[0].y, a0[0].z, a0[0].w};
+#pragma unroll
+    for (int sp = 1; sp < NL; ++sp)
+        if (NS || sp < nsplit) { acc[0] += a0[sp].x; acc[1] += a0[sp].y; acc[2] += a0[sp].z; acc[3] += a0[sp].w; }
+    auto un4 = [](uint2 v, float* f) {
+        f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+        f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+    };
+    float xi[4], wf[4], bf[4], xv[4];
+    un4(x0, xi);
+    un4(w0, wf);
+    un4(b0, bf);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) xv[e] = xi[e] + round_bf(acc[e]);
+    *reinterpret_cast<uint2*>(x_out + (size_t)row * D + c0) = make_uint2(pack2(xv[0], xv[1]), pack2(xv[2], xv[3]));
+    if (!ln_on_sum) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] = round_bf(xv[e]);
+    }
+    const int wv = t >> 6;
+    float sum = xv[0] + xv[1] + xv[2] + xv[3];
+    sum = wave_sum(sum);
+    if ((t & 63) == 0) red[wv] = sum;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tot += red[i];
+    const float mean = tot / (float)D;
+    float var = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { const float dd = xv[e] - mean; var += dd * dd; }
+    var = wave_sum(var);
+    if ((t & 63) == 0) red[8 + wv] = var;
+    __syncthreads();
+    float vt = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vt += red[8 + i];
+    const float rstd = 1.0f / sqrtf(vt / (float)D + eps);
+    const float nb = -rstd * mean;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(xv[e], rstd), nb), wf[e]), bf[e]);
+    *reinterpret_cast<uint2*>(xn_out + (size_t)row * D + c0) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+}
 template <bool NEOX>
 __global__ __launch_bounds__(256) void k_qkv_rope(const float* part, int nsplit, int R, int S, int H, int Hkv,
                                                   int hd, const float* freqs, int pos0, const int32_t* pos_dev,
@@ -513,6 +579,20 @@ extern "C" int zk_resid_ln(const float* part, int nsplit, const void* x_in, cons
         const char* e = getenv("ZK_RESID_D2K");
         return !(e && e[0] == '0');
     }();
+    // 512-thread rows (ZK_RL512=0: the 256-thread form; A/B knob, read once): 8 slabs 4.27 vs 4.41 us,
+    // c3 decode step 3.635 vs 3.646 ms (profiles/r2_s4_resid_ln_512_ab.txt)
+    static const bool rl512 = [] {
+        const char* e = getenv("ZK_RL512");
+        return !(e && e[0] == '0');
+    }();
+    if (D == 2048 && nsplit <= RL_MAXS && d2k && rl512) {
+        auto kern = nsplit == 4 ? k_resid_ln_d2k512<4> : nsplit == 8 ? k_resid_ln_d2k512<8> : k_resid_ln_d2k512<0>;
+        hipLaunchKernelGGL(kern, dim3(rows), dim3(512), 0, (hipStream_t)stream, part, nsplit, (const bf16_t*)x_in,
+                           (const bf16_t*)w, (const bf16_t*)b, eps, rows, (bf16_t*)x_out, (bf16_t*)xn_out, ln_on_sum,
+                           skip);
+        ZK_CHECK_LAUNCH("zk_resid_ln");
+        return 0;
+    }
     if (D == 2048 && nsplit <= RL_MAXS && d2k) {
         // exact-size instantiations for the split counts the engine uses (fewer load instructions)
         auto kern = nsplit == 1 ? k_resid_ln_d2k<1> : nsplit == 2 ? k_resid_ln_d2k<2> : nsplit == 4 ? k_resid_ln_d2k<4>
