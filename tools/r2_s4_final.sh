@@ -2,7 +2,7 @@
 # Round-2 session-4 evidence: full GPU tests, c3 (default) / c2 / c5 bench lines, c3 and c2 kernel stats
 set -e
 export TMPDIR=/tmp
-O=gpurun_out/s4final5
+O=gpurun_out/s4final6
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread > $O/tests.log 2>&1
 timeout -k 10 500 python -u bench.py > $O/bench_c3.log 2>&1
