@@ -13,8 +13,8 @@ batch. Other configs: --batch 1 --lc 160 --prefix 0 --new-tokens 861 (c2), --mod
 Multi-GPU: one process per GPU. `python bench.py --gpus N` starts torchrun itself (N ranks,
 127.0.0.1) before touching the GPU; under torchrun WORLD_SIZE must equal --gpus. Utterances
 are sharded by rank (row_base = rank * B keys the sampling noise), each rank runs its own
-engine with no data-path collective, and one RCCL all_gather of the int32 codes closes each
-step. Codes are shard-invariant as long as every shard has the same per-GPU batch (the GEMM
+engine with no data-path collective (zonos_amd.distributed.generate_sharded, the library
+path), and one RCCL all_gather of the int32 codes closes each generate. Codes are shard-invariant as long as every shard has the same per-GPU batch (the GEMM
 reduction order depends on the M regime). value = codes of all ranks /
 max-over-ranks wall time ("scaling": "weak").
 
@@ -174,29 +174,6 @@ def gemv_roofline(eng):
                  layers="rotating over all layers' fc1 weights")
 
 
-def step_small_roofline(eng, ctx):
-    """B <= 2 (c2): the persistent step kernel zk_decode_small (the whole backbone + norm_f + heads
-    of one decode step in one launch), launched back to back at the workload's mean context with
-    its own position word (the generate() state is left alone). Bytes per launch = every weight
-    once + the KV cache read at ctx + the new K/V rows (step_bytes)."""
-    import ctypes as C
-
-    import torch
-
-    from zonos_amd._lib import call
-    ws = eng._ws
-    R = ws["R"]
-    pos = torch.full((1,), ctx - 1, dtype=torch.int32, device=eng.device)
-    src = ws["small"]["args"]
-    args = type(src).from_buffer_copy(src)
-    args.pos_dev = pos.data_ptr()
-    args.skip = None
-    per = _time_launches([lambda st: call("zk_decode_small", C.byref(args), st)], reps=8)
-    eng._check_small(ws)
-    return _roof(step_bytes(eng, R, ctx), per, traffic=_pmc_traffic("k_decode_small", R=R, ctx=ctx),
-                 kernel="k_decode_small (zk_decode_small: persistent backbone + heads step)", M=R, ctx=ctx)
-
-
 def mamba_roofline(eng):
     """Hybrid (c5): zk_mamba_step (the SSM state update, HBM-bound) over every Mamba layer's state
     in turn; algorithmic bytes = SSM state read + write (R*d_inner*d_state*2 B each) + conv state
@@ -351,17 +328,20 @@ class GpuWorkload:
     def step(self, i, timed):
         torch, args = self.torch, self.args
         t0 = time.time()
-        codes = self.eng.generate(self.cond, self.prefix, args.new_tokens, 2.0, args.batch, self.sp, seed=1000 + i,
-                                  row_base=self.rank * args.batch, force_full_length=True, poll_every=64)
+        from zonos_amd.distributed import generate_sharded
+        # the library's sharded generate: this rank's B utterances of the global B x world batch
+        # (row_base = rank * B keys the noise), then one all_gather of the int32 codes
+        codes, allc = generate_sharded(self.eng, self.cond, self.prefix, args.new_tokens, 2.0,
+                                       args.batch * self.world, self.sp, seed=1000 + i, local_input=True,
+                                       coll_device=self.coll_dev, return_local=True, force_full_length=True,
+                                       poll_every=64)
+        assert len(codes) == args.batch and len(allc) == args.batch * self.world
         torch.cuda.synchronize(self.dev)
         t1 = time.time()
         if self.dac is not None:
             self.dac.decode_list(codes)
         torch.cuda.synchronize(self.dev)
         t2 = time.time()
-        if self.dist is not None:
-            from zonos_amd.distributed import gather_codes
-            gather_codes(codes, device=self.coll_dev)
         if timed:
             self.stats["gen_s"] += t1 - t0
             self.stats["dac_s"] += t2 - t1
@@ -377,8 +357,6 @@ class GpuWorkload:
         ctx_mean = args.lc + args.prefix + 1 + n_dec // 2
         if args.model == "hybrid":
             roof = mamba_roofline(eng)
-        elif "small" in eng._ws:
-            roof = step_small_roofline(eng, ctx_mean)
         elif eng._small(R):
             roof = gemv_roofline(eng)
         else:

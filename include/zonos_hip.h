@@ -114,63 +114,6 @@ int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, i
  * K = 2048 (16 heads x 128), nsplit in {2, 4, 8}. */
 int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const void* W, int M, int N, int K,
                      void* x, const int32_t* skip, void* stream);
-/* Persistent small-batch decode step (R = 2B <= 4 rows, Zonos-v0.1-transformer geometry:
- * D 2048, 16/4 heads x 128, FFN 8192): the whole backbone of one decode step
- * (zonos/backbone/_torch.py:99-102,117-152 for every layer, then norm_f and the 9 heads of
- * model.py:104-111) as ONE launch of one workgroup per CU. Each workgroup's loader wave streams
- * its share of every layer's weights (fragment-packed, 16 KB units) through an LDS ring by
- * LDS-DMA and runs ahead of the data dependencies; the consumer waves wait for each layer phase
- * (in_proj -> attention -> out_proj -> fc1 -> fc2) through agent-scope counters. Arithmetic is
- * that of the zk_gemv_fused launch sequence with 4 K-quarter waves and the unsplit fused decode
- * attention (bit-identical results). Outputs: heads logits as 4 K-quarter slabs p_heads
- * [4][R][n_heads_out] for zk_sample_heads(nsplit = 4). The caller zeroes `sync`
- * (zk_small_sync_words words) before the first step of a generate(); the kernel sets
- * sync[32] != 0 if a dependency wait gave up (never in a correct run). */
-typedef struct zk_small_layer {
-    const void* wqkv;       /* in_proj, packed [3072][2048] */
-    const void* wo;         /* out_proj, packed [2048][2048] */
-    const void* fc1;        /* fc1, zk_permute_fc1 order, packed [16384][2048] */
-    const void* fc2;        /* fc2, packed [2048][8192] */
-    const void* ln1_w;
-    const void* ln1_b;
-    const void* ln2_w;
-    const void* ln2_b;
-    void* k_cache;          /* this layer's K cache [R][4][Smax x 128] (fragment order) */
-    void* vt_cache;         /* V^T cache, same shape */
-} zk_small_layer;
-typedef struct zk_small_args {
-    const zk_small_layer* layers;   /* DEVICE array of n_layer entries */
-    int32_t n_layer;
-    int32_t R;                      /* rows = 2 x batch (CFG), 1..4 */
-    int32_t Smax;                   /* KV cache keys per (row, kv head), multiple of 256 */
-    int32_t n_heads_out;            /* 9 x 1026 */
-    const void* heads;              /* packed stacked heads [n_heads_out -> pad 64][2048] */
-    const void* lnf_w;
-    const void* lnf_b;
-    float eps;
-    const float* freqs;             /* RoPE table [pos][64][2] */
-    const int32_t* pos_dev;         /* device: position of the new token (= context - 1) */
-    void* x;                        /* bf16 [R][2048] layer input (embedding on entry) */
-    void* xm;                       /* bf16 [R][2048] residual after attention */
-    float* p_qkv;                   /* fp32 [4][R][3072] in_proj K-quarter partials */
-    void* y;                        /* bf16 [R][2048] attention output */
-    float* p_o;                     /* fp32 [4][R][2048] */
-    void* h;                        /* bf16 [R][8192] SwiGLU output */
-    float* p_f;                     /* fp32 [4][R][2048] */
-    float* p_heads;                 /* fp32 [4][R][n_heads_out] */
-    uint32_t* sync;                 /* zk_small_sync_words(n_layer) words */
-    const int32_t* skip;            /* device: nonzero = generation finished, no-op */
-    int32_t attn_splits;            /* key splits per (row, kv head), merged in the launch */
-    float* attn_work;               /* fp32 [R][4][attn_splits][8 + 4 x 128] split partials */
-    uint64_t* prof;                 /* nullable: per-workgroup phase timestamps (s_memrealtime,
-                                       100 MHz) [ncu][n_layer * 5 + 2][4] -- profiling only */
-} zk_small_args;
-int zk_small_sync_words(int n_layer);
-/* Cache warming (tuning experiments): read nseg segments of seg_bytes at stride seg_stride with
- * the given policy (0 plain, 1 non-temporal) and discard them, leaving them in the Infinity Cache. */
-int zk_prefetch(const void* base, long seg_stride, long seg_bytes, int nseg, int mode, int nblocks,
-                uint32_t* sink, void* stream);
-int zk_decode_small(const zk_small_args* a, void* stream);
 /* fc1 weight [2F][D] (rows: F "y" then F "gate") -> interleaved groups of 8 y + 8 gate rows. */
 int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream);
 /* nn.Linear weight [N][K] bf16 -> fragment-packed [ceil64(N)/16][K/32][64][8] (rows >= N zero):

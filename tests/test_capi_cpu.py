@@ -121,18 +121,15 @@ def test_struct_layouts_match_header(tmp_path):
 
 def test_ctypes_struct_layouts_match_the_c_abi(lib):
     """The by-value / by-pointer ABI structs the Python binding builds (SamplingParams, GenState,
-    SmallLayer, SmallArgs, ZkCondSeg, ZkCondPlan) have the C compiler's size and field offsets."""
+    ZkCondSeg, ZkCondPlan, StepLayer, StepDesc, DacDesc) have the C compiler's size and field offsets."""
     import ctypes as C
 
     from zonos_amd import _lib
     from zonos_amd.conditioning import ZkCondPlan, ZkCondSeg
     lib.zk_abi_size.restype = C.c_long
     lib.zk_abi_size.argtypes = [C.c_int]
-    for which, cls in enumerate([_lib.SamplingParams, _lib.GenState, _lib.SmallLayer, _lib.SmallArgs, ZkCondSeg,
-                                 ZkCondPlan]):
+    for which, cls in [(0, _lib.SamplingParams), (1, _lib.GenState), (4, ZkCondSeg), (5, ZkCondPlan)]:
         assert lib.zk_abi_size(which) == C.sizeof(cls), (cls.__name__, lib.zk_abi_size(which), C.sizeof(cls))
-    assert lib.zk_abi_size(10) == _lib.SmallArgs.prof.offset
-    assert lib.zk_abi_size(11) == _lib.SmallArgs.eps.offset
     assert lib.zk_abi_size(12) == _lib.GenState.seed.offset
     assert lib.zk_abi_size(6) == C.sizeof(_lib.StepLayer) and lib.zk_abi_size(7) == C.sizeof(_lib.StepDesc)
     assert lib.zk_abi_size(13) == _lib.StepDesc.eps.offset
@@ -141,14 +138,3 @@ def test_ctypes_struct_layouts_match_the_c_abi(lib):
     assert lib.zk_abi_size(16) == _lib.DacDesc.blocks.offset
 
 
-def test_persistent_step_selection():
-    """zk_decode_small is opt-in (ZK_PERSIST=1) and only for R <= 4 at the Zonos-v0.1 geometry."""
-    from zonos_amd.engine import EngineConfig, HipDecoder
-    assert HipDecoder.persistent_small in (False, True)
-    eng = HipDecoder.__new__(HipDecoder)
-    eng.cfg = EngineConfig(d_model=2048, n_layer=26, n_heads=16, n_kv=4, d_ff=8192)
-    eng.rope_neox = 0
-    eng.persistent_small = True
-    assert eng._persist(2) and eng._persist(4) and not eng._persist(8)
-    eng.cfg = EngineConfig(d_model=256, n_layer=2, n_heads=4, n_kv=2, d_ff=512)
-    assert not eng._persist(2)

@@ -36,3 +36,24 @@ def test_backbone_plugin_parameter_layout():
     got = {k: tuple(v.shape) for k, v in bb.state_dict().items()}
     exp = {k[len("backbone."):]: v for k, v in zonos_ref.weight_shapes(TINY).items() if k.startswith("backbone.")}
     assert got == exp
+
+
+def test_pad_weight_matches_reference_branches():
+    """zonos.utils.pad_weight_ follows utils.py:22-37 branch for branch: Embedding tested on
+    embedding_dim (so Embedding(1026, 2048) stays), Linear padded on out_features
+    (1025 -> 1026, in_features kept), both dims reset, other modules raise ValueError."""
+    import pytest
+    from zonos.utils import pad_weight_
+    e = torch.nn.Embedding(1026, 2048)
+    pad_weight_(e, 8)
+    assert tuple(e.weight.shape) == (1026, 2048) and (e.num_embeddings, e.embedding_dim) == (1026, 2048)
+    e2 = torch.nn.Embedding(1024, 2045)      # 2045 % 8 = 5 -> +5 rows (the reference's quirk)
+    pad_weight_(e2, 8)
+    assert tuple(e2.weight.shape) == (1029, 2045) and (e2.num_embeddings, e2.embedding_dim) == (1029, 2045)
+    lin = torch.nn.Linear(2048, 1025)
+    w0 = lin.weight.detach().clone()
+    pad_weight_(lin, 8)
+    assert tuple(lin.weight.shape) == (1026, 2048) and (lin.out_features, lin.in_features) == (1026, 2048)
+    assert torch.equal(lin.weight[:1025], w0) and not lin.weight[1025].any()
+    with pytest.raises(ValueError):
+        pad_weight_(torch.nn.Conv1d(2, 2, 1), 8)

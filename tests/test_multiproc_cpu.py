@@ -50,3 +50,72 @@ def test_gather_codes_gloo_world2():
     for p in ps:
         p.join(timeout=60)
     assert all(ok for _, ok in res), res
+
+
+class StubEngine:
+    """Stands in for HipDecoder.generate: utterance b's codes are a function of its global index
+    (row_base + b), the seed and ITS cond / uncond rows only, as the real engine's are."""
+
+    def generate(self, cond, prefix, max_new, cfg_scale, B, sp, *, seed, row_base=0, **kw):
+        assert cond.shape[0] == 2 * B and (prefix is None or prefix.shape[0] == B)
+        out = []
+        for b in range(B):
+            g = row_base + b
+            v = int(cond[b, 0, 0]) * 1000 + int(cond[B + b, 0, 0]) + (seed % 97) + (0 if prefix is None else int(prefix[b, 0, 0]))
+            out.append(torch.full((9, 2 + g % 3), v % 1024, dtype=torch.int64))
+        return out
+
+
+def _global_inputs(B):
+    cond = torch.zeros(2 * B, 3, 4)
+    cond[:B, 0, 0] = torch.arange(B).float()            # cond row i carries i
+    cond[B:, 0, 0] = 100 + torch.arange(B).float()      # its uncond partner carries 100 + i
+    prefix = torch.arange(B).view(B, 1, 1).expand(B, 9, 2).clone()
+    return cond, prefix
+
+
+def _sharded_worker(rank, world, port, q):
+    from zonos_amd.distributed import generate_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(1234 + rank)                      # differs per rank: seed=None must be broadcast
+    B = 5
+    cond, prefix = _global_inputs(B)
+    got = generate_sharded(StubEngine(), cond, prefix, 8, 2.0, B, {}, coll_device="cpu")
+    ref = StubEngine().generate(cond, prefix, 8, 2.0, B, {}, seed=0, row_base=0)
+    # same codes as one batch up to the seed term, which every rank must share
+    seeds = {int(a[0, 0] - b[0, 0]) % 1024 for a, b in zip(got, ref)}
+    ok = len(got) == B and len(seeds) == 1 and all(a.shape == b.shape for a, b in zip(got, ref))
+    # explicit seed, rank-local inputs, no gather
+    rb, n = shard(B, world, rank)
+    loc = torch.cat([cond[rb:rb + n], cond[B + rb:B + rb + n]])
+    mine = generate_sharded(StubEngine(), loc, prefix[rb:rb + n], 8, 2.0, B, {}, seed=7, gather=False,
+                            local_input=True, coll_device="cpu")
+    ref7 = StubEngine().generate(cond, prefix, 8, 2.0, B, {}, seed=7)[rb:rb + n]
+    ok = ok and len(mine) == n and all(torch.equal(a, b) for a, b in zip(mine, ref7))
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_generate_sharded_gloo_world2():
+    """generate_sharded over 2 gloo ranks (B = 5: ragged 3 + 2 shards) returns the one-batch codes
+    in global order on every rank; seed=None is drawn once and broadcast."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(ok for _, ok in res), res
+
+
+def test_generate_sharded_single_process():
+    from zonos_amd.distributed import generate_sharded
+    cond, prefix = _global_inputs(4)
+    got = generate_sharded(StubEngine(), cond, prefix, 8, 2.0, 4, {}, seed=3)
+    ref = StubEngine().generate(cond, prefix, 8, 2.0, 4, {}, seed=3)
+    assert all(torch.equal(a, b) for a, b in zip(got, ref))

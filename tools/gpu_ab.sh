@@ -1,0 +1,53 @@
+#!/bin/bash
+# One parametrised A/B / evidence driver for GPU boxes (replaces the round-1/2 one-off scripts).
+#
+#   tools/gpu_ab.sh OUT STEP [STEP ...]
+#
+# OUT is a directory under gpurun_out/. Each STEP runs under its own time limit, steps are
+# chained (the first failure ends the run):
+#   tests[:PYTEST_K]      pytest -m gpu (optionally -k PYTEST_K)
+#   bench:NAME[:ARGS]     bench.py ARGS (comma-separated) -> OUT/bench_NAME.json.log
+#   micro:MODE            tools/microbench.py MODE on the product library and every
+#                         zonos_amd/lib/variants/<v> (built on the CPU with
+#                         zonos_amd.build.build_variant), twice, interleaved
+#   prof:NAME[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> OUT/prof_NAME/*stats.csv
+#   pmc:NAME:COUNTERS[:ARGS]  one rocprofv3 --pmc pass (COUNTERS comma-separated, within one
+#                         block's limits) of bench.py ARGS -> OUT/pmc_NAME/
+set -e
+export TMPDIR=/tmp
+OUT=gpurun_out/$1
+shift
+mkdir -p "$OUT"
+for step in "$@"; do
+  kind=${step%%:*}; rest=${step#*:}; [ "$rest" = "$step" ] && rest=""
+  case "$kind" in
+    tests)
+      k=(); [ -n "$rest" ] && k=(-k "$rest")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
+          > "$OUT/tests.log" 2>&1
+      tail -n 1 "$OUT/tests.log" ;;
+    bench)
+      name=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      timeout -k 10 600 python -u bench.py ${a//,/ } > "$OUT/bench_$name.json.log" 2>&1
+      grep '^{' "$OUT/bench_$name.json.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['value'], d['unit'], d.get('breakdown'))" ;;
+    micro)
+      for i in 1 2; do
+        echo "== product"; timeout -k 10 180 python tools/microbench.py $rest
+        for v in $(ls zonos_amd/lib/variants 2>/dev/null); do
+          echo "== $v"; ZK_LIB_PATH=zonos_amd/lib/variants/$v/libzonos_hip.so timeout -k 10 180 python tools/microbench.py $rest
+        done
+      done > "$OUT/micro_$rest.log" 2>&1
+      grep -v amdgpu "$OUT/micro_$rest.log" ;;
+    prof)
+      name=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
+          python3 bench.py ${a//,/ } > "$OUT/prof_$name.log" 2>&1
+      find "$OUT/prof_$name" -type f ! -name "*stats.csv" -delete ;;
+    pmc)
+      name=${rest%%:*}; r2=${rest#*:}; ctr=${r2%%:*}; a=${r2#*:}; [ "$a" = "$r2" ] && a=""
+      timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "$OUT/pmc_$name" -o run -- \
+          python3 bench.py ${a//,/ } > "$OUT/pmc_$name.log" 2>&1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+du -sh "$OUT"

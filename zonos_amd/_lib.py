@@ -35,18 +35,6 @@ class GenState(C.Structure):
                 ("seed", U64), ("row_base", C.c_int32)]
 
 
-class SmallLayer(C.Structure):
-    _fields_ = [("wqkv", P), ("wo", P), ("fc1", P), ("fc2", P), ("ln1_w", P), ("ln1_b", P), ("ln2_w", P),
-                ("ln2_b", P), ("k_cache", P), ("vt_cache", P)]
-
-
-class SmallArgs(C.Structure):
-    _fields_ = [("layers", P), ("n_layer", C.c_int32), ("R", C.c_int32), ("Smax", C.c_int32),
-                ("n_heads_out", C.c_int32), ("heads", P), ("lnf_w", P), ("lnf_b", P), ("eps", F), ("freqs", P),
-                ("pos_dev", P), ("x", P), ("xm", P), ("p_qkv", P), ("y", P), ("p_o", P), ("h", P), ("p_f", P),
-                ("p_heads", P), ("sync", P), ("skip", P), ("attn_splits", C.c_int32), ("attn_work", P), ("prof", P)]
-
-
 class StepLayer(C.Structure):
     _fields_ = [("ln1_w", P), ("ln1_b", P), ("wqkv", P), ("wo", P), ("ln2_w", P), ("ln2_b", P), ("fc1", P),
                 ("fc2", P), ("k_cache", P), ("vt_cache", P)]
@@ -91,8 +79,6 @@ _SIGS = {
     "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, I, P, P],
     "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
     "zk_gemv_fused": [P, L, P, I, I, I, I, P, P, F, P, P, P, P],
-    "zk_decode_small": [C.POINTER(SmallArgs), P],
-    "zk_prefetch": [P, L, L, I, I, I, P, P],
     "zk_permute_fc1": [P, I, I, P, P],
     "zk_pack_weights": [P, I, I, P, P],
     "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, I, P, P],
@@ -159,8 +145,6 @@ def load():
     lib.zk_last_error.argtypes = []
     lib.zk_loudness_max_blocks.restype = C.c_int
     lib.zk_loudness_max_blocks.argtypes = [L, I]
-    lib.zk_small_sync_words.restype = C.c_int
-    lib.zk_small_sync_words.argtypes = [I]
     lib.zk_abi_size.restype = C.c_long
     lib.zk_abi_size.argtypes = [I]
     lib.zk_dac_decode_workspace.restype = C.c_size_t
@@ -170,7 +154,7 @@ def load():
 
 
 def exported_symbols() -> list[str]:
-    return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_small_sync_words", "zk_abi_size",
+    return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_abi_size",
                           "zk_dac_decode_workspace"]
 
 

@@ -171,9 +171,9 @@ class HipDacDecoder:
         cl["conv2_w"], cl["conv2_b"] = cw.contiguous(), self.conv2_b.contiguous()
         self.cl = cl
 
-    # the decode's launch sequence is enqueued by the C ABI (zk_dac_decode); ZK_C_DAC=0 issues the
+    # the decode's launch sequence is enqueued by the C ABI (zk_dac_decode); False issues the
     # same sequence from Python (bit-identical; the reference for the test)
-    c_dac = os.environ.get("ZK_C_DAC", "1") != "0"
+    c_dac = True
 
     def _dac_desc(self):
         if getattr(self, "_desc", None) is None:

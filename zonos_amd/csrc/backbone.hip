@@ -220,85 +220,10 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
     ln_row_pre<LN_NT, N8>(xv, wv, bv, eps, D, xn_out + (size_t)row * D, red);
 }
 
-// k_resid_ln for D = 2048 with whole-line slab reads: thread t owns the float4 pieces t and
-// t + 256 of the row, so every fp32 slab load instruction of a wave reads 1 KB contiguous (the
-// 8-element-per-thread layout of k_resid_ln reads 16 B of every 32 B per instruction, each
-// line twice). Same arithmetic per element; the LayerNorm sums group the elements differently.
+// k_resid_ln for D = 2048 with whole-line slab reads: 512 threads, thread t owns float4 piece t of
+// the row, so every fp32 slab load instruction of a wave reads 1 KB contiguous; all slab loads of
+// a row are issued before the first add (one memory round trip); LayerNorm sums over 8 waves.
 // NS > 0: exactly NS slabs (only real slabs loaded); NS = 0: nsplit <= RL_MAXS with clamped loads
-template <int NS>
-__global__ __launch_bounds__(LN_NT) void k_resid_ln_d2k(const float* part, int nsplit, const bf16_t* x_in,
-                                                        const bf16_t* w, const bf16_t* b, float eps, int rows,
-                                                        bf16_t* x_out, bf16_t* xn_out, int ln_on_sum,
-                                                        const int32_t* skip) {
-    constexpr int D = 2048;
-    __shared__ float red[2 * LN_NT / 64];
-    if (skip && *skip) return;
-    const int row = blockIdx.x, t = threadIdx.x;
-    const size_t slab = (size_t)rows * D;
-    const int c0 = 4 * t, c1 = 1024 + 4 * t;
-    // one memory round trip: LN weights, residual and every slab issued before the first add
-    const uint2 w0 = *reinterpret_cast<const uint2*>(w + c0), w1 = *reinterpret_cast<const uint2*>(w + c1);
-    const uint2 b0 = *reinterpret_cast<const uint2*>(b + c0), b1 = *reinterpret_cast<const uint2*>(b + c1);
-    const uint2 x0 = *reinterpret_cast<const uint2*>(x_in + (size_t)row * D + c0);
-    const uint2 x1 = *reinterpret_cast<const uint2*>(x_in + (size_t)row * D + c1);
-    const float* p = part + (size_t)row * D;
-    constexpr int NL = NS ? NS : RL_MAXS;
-    float4 a0[NL], a1[NL];
-#pragma unroll
-    for (int sp = 0; sp < NL; ++sp) {
-        const float* ps = p + (size_t)(NS ? sp : min(sp, nsplit - 1)) * slab;
-        a0[sp] = *reinterpret_cast<const float4*>(ps + c0);
-        a1[sp] = *reinterpret_cast<const float4*>(ps + c1);
-    }
-    float acc[8] = {a0[0].x, a0[0].y, a0[0].z, a0[0].w, a1[0].x, a1[0].y, a1[0].z, a1[0].w};
-#pragma unroll
-    for (int sp = 1; sp < NL; ++sp)
-        if (NS || sp < nsplit) {
-            acc[0] += a0[sp].x; acc[1] += a0[sp].y; acc[2] += a0[sp].z; acc[3] += a0[sp].w;
-            acc[4] += a1[sp].x; acc[5] += a1[sp].y; acc[6] += a1[sp].z; acc[7] += a1[sp].w;
-        }
-    auto un4 = [](uint2 v, float* f) {
-        f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-        f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-    };
-    float xi[8], wf[8], bf[8], xv[8];
-    un4(x0, xi); un4(x1, xi + 4);
-    un4(w0, wf); un4(w1, wf + 4);
-    un4(b0, bf); un4(b1, bf + 4);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) xv[e] = xi[e] + round_bf(acc[e]);      // x = bf16(x + bf16(proj))
-    *reinterpret_cast<uint2*>(x_out + (size_t)row * D + c0) = make_uint2(pack2(xv[0], xv[1]), pack2(xv[2], xv[3]));
-    *reinterpret_cast<uint2*>(x_out + (size_t)row * D + c1) = make_uint2(pack2(xv[4], xv[5]), pack2(xv[6], xv[7]));
-    if (!ln_on_sum) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xv[e] = round_bf(xv[e]);
-    }
-    const int wv = t >> 6;
-    float sum = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sum += xv[e];
-    sum = wave_sum(sum);
-    if ((t & 63) == 0) red[wv] = sum;
-    __syncthreads();
-    const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
-    float var = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { const float d = xv[e] - mean; var += d * d; }
-    var = wave_sum(var);
-    if ((t & 63) == 0) red[4 + wv] = var;
-    __syncthreads();
-    const float rstd = 1.0f / sqrtf((red[4] + red[5] + red[6] + red[7]) / (float)D + eps);
-    const float nb = -rstd * mean;
-    float o[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(xv[e], rstd), nb), wf[e]), bf[e]);
-    *reinterpret_cast<uint2*>(xn_out + (size_t)row * D + c0) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-    *reinterpret_cast<uint2*>(xn_out + (size_t)row * D + c1) = make_uint2(pack2(o[4], o[5]), pack2(o[6], o[7]));
-}
-
-
-// 512-thread form of k_resid_ln_d2k (default; ZK_RL512=0 selects the 256-thread form): thread t owns float4 piece t of the row,
-// so each wave issues half the slab loads; LayerNorm sums over 8 waves
 template <int NS>
 __global__ __launch_bounds__(512) void k_resid_ln_d2k512(const float* part, int nsplit, const bf16_t* x_in,
                                                          const bf16_t* w, const bf16_t* b, float eps, int rows,
@@ -575,31 +500,13 @@ extern "C" int zk_resid_ln(const float* part, int nsplit, const void* x_in, cons
     ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_resid_ln: unsupported D=%d", D);
     ZK_REQUIRE(nsplit >= 1, "zk_resid_ln: nsplit must be >= 1");
     if (rows == 0) return 0;
-    static const bool d2k = [] {               // ZK_RESID_D2K=0: generic layout (A/B knob, read once)
-        const char* e = getenv("ZK_RESID_D2K");
-        return !(e && e[0] == '0');
-    }();
-    // 512-thread rows (ZK_RL512=0: the 256-thread form; A/B knob, read once): 8 slabs 4.27 vs 4.41 us,
-    // c3 decode step 3.635 vs 3.646 ms (profiles/r2_s4_resid_ln_512_ab.txt)
-    static const bool rl512 = [] {
-        const char* e = getenv("ZK_RL512");
-        return !(e && e[0] == '0');
-    }();
-    if (D == 2048 && nsplit <= RL_MAXS && d2k && rl512) {
+    // D = 2048: 512-thread rows (8 slabs 4.27 vs 4.41 us with 256 threads x 2 pieces, c3 decode
+    // step 3.635 vs 3.646 ms, profiles/r2_s4_resid_ln_512_ab.txt)
+    if (D == 2048 && nsplit <= RL_MAXS) {
         auto kern = nsplit == 4 ? k_resid_ln_d2k512<4> : nsplit == 8 ? k_resid_ln_d2k512<8> : k_resid_ln_d2k512<0>;
         hipLaunchKernelGGL(kern, dim3(rows), dim3(512), 0, (hipStream_t)stream, part, nsplit, (const bf16_t*)x_in,
                            (const bf16_t*)w, (const bf16_t*)b, eps, rows, (bf16_t*)x_out, (bf16_t*)xn_out, ln_on_sum,
                            skip);
-        ZK_CHECK_LAUNCH("zk_resid_ln");
-        return 0;
-    }
-    if (D == 2048 && nsplit <= RL_MAXS && d2k) {
-        // exact-size instantiations for the split counts the engine uses (fewer load instructions)
-        auto kern = nsplit == 1 ? k_resid_ln_d2k<1> : nsplit == 2 ? k_resid_ln_d2k<2> : nsplit == 4 ? k_resid_ln_d2k<4>
-                  : nsplit == 8 ? k_resid_ln_d2k<8> : k_resid_ln_d2k<0>;
-        hipLaunchKernelGGL(kern, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, part, nsplit,
-                           (const bf16_t*)x_in, (const bf16_t*)w, (const bf16_t*)b, eps, rows, (bf16_t*)x_out,
-                           (bf16_t*)xn_out, ln_on_sum, skip);
         ZK_CHECK_LAUNCH("zk_resid_ln");
         return 0;
     }

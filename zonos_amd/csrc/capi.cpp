@@ -24,18 +24,14 @@ extern "C" const char* zk_last_error(void) { return g_err; }
 extern "C" int zk_version(void) { return 1; }
 
 // sizeof / offsetof of the by-value ABI structs, so a binding (ctypes here) can verify its
-// layout without a GPU: which = 0 zk_sampling_params, 1 zk_gen_state, 2 zk_small_layer,
-// 3 zk_small_args, 4 ZkCondSeg, 5 ZkCondPlan; 10 + k = offset of zk_small_args' last field (prof).
+// layout without a GPU: which = 0 zk_sampling_params, 1 zk_gen_state, 4 ZkCondSeg, 5 ZkCondPlan,
+// 6 zk_step_layer, 7 zk_step_desc, 8 zk_dac_desc; 12-17 field offsets (see the cases).
 extern "C" long zk_abi_size(int which) {
     switch (which) {
         case 0: return (long)sizeof(zk_sampling_params);
         case 1: return (long)sizeof(zk_gen_state);
-        case 2: return (long)sizeof(zk_small_layer);
-        case 3: return (long)sizeof(zk_small_args);
         case 4: return (long)sizeof(ZkCondSeg);
         case 5: return (long)sizeof(ZkCondPlan);
-        case 10: return (long)offsetof(zk_small_args, prof);
-        case 11: return (long)offsetof(zk_small_args, eps);
         case 12: return (long)offsetof(zk_gen_state, seed);
         case 6: return (long)sizeof(zk_step_layer);
         case 7: return (long)sizeof(zk_step_desc);

@@ -80,10 +80,6 @@ ZK_DEV void wait_vm(int n) {
 
 constexpr int CL_DA = 3;                 // weight slices in flight ahead of the step being computed
 constexpr int CL_NW = CL_DA + 2;         // weight ring slots
-#ifndef ZK_CL_DEEP_DA
-#define ZK_CL_DEEP_DA 8
-#endif
-constexpr int CL_DEEP_DA = ZK_CL_DEEP_DA; // deep form: weight slices in flight
 constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 
 // Loader-wave implicit GEMM. Wave 4 only moves bytes (LDS-DMA) and counts its own vmcnt;
@@ -92,7 +88,7 @@ constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 // Step i = (chunk c, tap t); the loader runs CL_DA steps ahead for weights and DX steps
 // ahead for windows (DX >= CL_DA, window ring of NX slots), one raw s_barrier per step.
 // DA: weight slices the loader keeps in flight (ring of DA + 2 slots); OCC: workgroups per CU the
-// registers are sized for (the deep form runs one workgroup per CU with a 2.7x deeper weight ring)
+// registers are sized for
 template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2>
 __global__ __launch_bounds__(CL_THREADS, OCC) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
@@ -447,24 +443,6 @@ __global__ __launch_bounds__(256) void k_rvq_encode(const float* __restrict__ z,
     }
 }
 
-// ZK_DAC_WIDE=0 keeps 128-position tiles everywhere (A/B knob, read once)
-bool dac_wide_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ZK_DAC_WIDE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// ZK_DAC_DEEP=1: plain k7 convs in the deep form (A/B knob, read once; default off)
-bool dac_deep_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ZK_DAC_DEEP");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 template <int FM, int NQ, int DA = CL_DA, int OCC = 2>
 void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Cin, int Tin, const uint16_t* w,
                  long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
@@ -537,17 +515,14 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     // convs, overhead-bound at 128: -6 % / -15 %); the residual convs keep 128 (their prefetched
     // residual tile would not fit the registers beside twice the accumulators), and so do the
     // polyphase ConvTranspose convs (+12-22 % with 256, profiles/r1_dac_wide_tiles_ab.txt)
-    // deep (ZK_DAC_DEEP, tuning): the plain k7 convs as one workgroup per CU with 256-position
-    // tiles and CL_DEEP_DA weight slices in flight (the LDS-DMA weight stream is latency-bound at
-    // CL_DA = 3 with two workgroups per CU)
-    const bool deep = resid == nullptr && !s_f32 && nphase == 1 && ks > 1 && dac_deep_enabled();
-    const bool wide = deep || (resid == nullptr && !s_f32 && nphase == 1 && FM <= 3 && dac_wide_enabled());
+    // (one workgroup per CU with a deeper weight ring measured slower: DESIGN.md §6)
+    const bool wide = resid == nullptr && !s_f32 && nphase == 1 && FM <= 3;
     const int qt = wide ? 2 * QT : QT;
     const int win = qt + (ks - 1) * dil;
     const size_t xs = (size_t)((win + 15) / 16) * 1024;
     const size_t ws = (size_t)32 * FM * 64;
-    const int da = deep ? CL_DEEP_DA : CL_DA;
-    const size_t lds_cap = deep ? 160 * 1024 : 80 * 1024;
+    const int da = CL_DA;
+    const size_t lds_cap = 80 * 1024;
     // window lead DX >= da steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
     int dx = std::max(da, ks), nx = 1 + (dx + 1 + ks - 1) / ks;
     while (dx > da && (da + 2) * ws + nx * xs > lds_cap) {
@@ -564,21 +539,6 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     launch_conv<F_, NQ_>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad, Qn, nphase, \
                          out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32, lens, in_scale, out_scale, nq, \
                          nx, dx)
-#define ZK_CLD(F_)                                                                                                \
-    launch_conv<F_, 8, CL_DEEP_DA, 1>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad,  \
-                                     Qn, nphase, out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32,  \
-                                     lens, in_scale, out_scale, nq, nx, dx)
-    if (deep) {
-        switch (FM) {
-            case 4: ZK_CLD(4); break;
-            case 3: ZK_CLD(3); break;
-            case 2: ZK_CLD(2); break;
-            default: ZK_CLD(1); break;
-        }
-        ZK_CHECK_LAUNCH("zk_dac_conv_cl");
-        return 0;
-    }
-#undef ZK_CLD
     switch (FM) {
         case 4: ZK_CL(4, 4); break;
         case 3: if (wide) ZK_CL(3, 8); else ZK_CL(3, 4); break;

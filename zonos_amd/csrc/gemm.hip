@@ -18,6 +18,7 @@
 //
 // mode 0: fp32 partial slabs; mode 1: fused SwiGLU for FeedForward.fc1 (_torch.py:150-152).
 #include "common.h"
+#include "attn_common.h"
 #include "../../include/zonos_hip.h"
 #include <algorithm>
 #include <stdlib.h>
@@ -29,7 +30,6 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int BM = 128, BN = 64, BK = 64, NT = 256;
 
-ZK_DEV bf16x8 as_frag(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 // streamed-once weights: non-temporal 16-byte load (global_load_dwordx4 ... nt)
@@ -601,7 +601,8 @@ constexpr int GF_XS = 2048 + 8;    // LDS row stride (bf16) of the LayerNorm'd r
 // ranges -- the [row][kv head][split] (m, l, O) partials of zk_attn_decode_qkv_part in `mw` --
 // and the prologue merges them exactly as k_attn_combine does (backbone.hip) into LDS; each
 // wave merges the 2 heads of its own K range (K = 2048, NW = 8), rows < M <= 2.
-constexpr int GF_AT_G = 4, GF_AT_STR = 2 * GF_AT_G + GF_AT_G * 128;    // = AT_G, AT_STR (attn_common.h)
+constexpr int GF_AT_G = AT_G, GF_AT_STR = AT_STR;    // the partials layout of attn_common.h (one definition)
+static_assert(GF_AT_STR == 2 * GF_AT_G + GF_AT_G * 128, "attention partials layout");
 // XR: rows the LDS activation image holds (2 for B = 1, 16 otherwise): a 16-row image is 66 KB and
 // caps the LayerNorm-prologue GEMVs at 2 workgroups per CU; the 2-row image (8 KB) does not.
 #ifndef ZK_GF_OCC2
@@ -866,24 +867,6 @@ __global__ void k_permute_fc1(const bf16_t* w, int F, int D, bf16_t* out) {
     for (int i = threadIdx.x; i < D / 8; i += blockDim.x) d[i] = s[i];
 }
 
-// ZK_PREFILL_NTW=1 keeps one 16-column tile per wave in the large-M GEMM (A/B knob, read once)
-bool prefill_ntw2() {
-    static const bool on = [] {
-        const char* e = getenv("ZK_PREFILL_NTW");
-        return !(e && e[0] == '1');
-    }();
-    return on;
-}
-
-// ZK_GEMV=0 disables the small-M weight-stream GEMV (A/B tuning knob, read once)
-bool gemv_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("ZK_GEMV");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 }  // namespace
 
 extern "C" int zk_pack_weights(const void* w, int N, int K, void* out, void* stream) {
@@ -904,7 +887,7 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemm_bf16: lda=%ld", lda);
     ZK_REQUIRE(mode == 0 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_bf16: bad mode/nsplit");
     const int nchunks = K / nsplit / BK;
-    if (M <= 16 && gemv_enabled() && (K / nsplit) % 128 == 0) {
+    if (M <= 16 && (K / nsplit) % 128 == 0) {
         // weight-stream GEMV (B <= 8 decode): 2 column tiles per workgroup, K quarters per wave
         const int ks = K / nsplit / 128;
         dim3 g((N + 31) / 32, 1, nsplit);
@@ -991,7 +974,7 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     }
     // large M (prefill): two 16-column tiles per wave for the slab GEMMs (c3 prefill: in_proj
     // 1.01 vs 1.09 ms, fc2 1.98 vs 2.29 ms; the SwiGLU fc1 is faster with one: 4.87 vs 5.24 ms)
-    const int ntw = (prefill_ntw2() && mode == 0 && M > BM && N >= 8 * BN) ? 2 : 1;
+    const int ntw = (mode == 0 && M > BM && N >= 8 * BN) ? 2 : 1;
     dim3 grid((N + BN * ntw - 1) / (BN * ntw), (M + BM - 1) / BM, nsplit);
     const int U = (nchunks % 4 == 0) ? 4 : (nchunks % 2 == 0 ? 2 : 1);
 #define ZK_GEMM_LAUNCH(MODE_, U_)                                                                         \
@@ -1015,17 +998,6 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
     return 0;
 }
 
-namespace {
-// ZK_GF_XR2=0: 16-row LDS image at B = 1 too (A/B knob, read once)
-bool gf_xr2() {
-    static const bool on = [] {
-        const char* e = getenv("ZK_GF_XR2");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-}  // namespace
-
 extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, int mode,
                              const void* ln_w, const void* ln_b, float eps, float* Cf, void* Cb,
                              const int32_t* skip_flag, void* stream) {
@@ -1043,16 +1015,6 @@ extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int 
     // tiles (in_proj, N = 3072: 192 workgroups, 6.5 vs 7.5 us with half tiles at B = 1 --
     // the prologue's latency, not the weight stream, sets its time; tools/gemv_probe.sh)
     int lay = (mode != 1 && tiles < 256 && !ln_w) ? 0 : (tiles >= 512 ? 2 : 1);
-    static const int lay_force = [] {       // tuning knob (not used by default): 0 half, 1 one, 2 two tiles
-        const char* e = getenv("ZK_GF_LAYOUT");
-        return e ? atoi(e) : -1;
-    }();
-    if (lay_force >= 0 && !(lay_force == 0 && mode == 1)) lay = lay_force;
-    static const bool b1_lay1 = [] {      // B = 1: one tile per workgroup for the wide LN GEMVs (fc1, heads)
-        const char* e = getenv("ZK_GF_B1_LAY1");
-        return e && e[0] == '1';
-    }();
-    if (lay_force < 0 && b1_lay1 && M <= 2 && ln_w && lay == 2) lay = 1;
     const int grid = lay == 0 ? 2 * tiles : (lay == 2 ? (tiles + 1) / 2 : tiles);
     const bool ln = ln_w != nullptr;
     (void)ln;
@@ -1074,7 +1036,7 @@ extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int 
     do {                                                                                                      \
         constexpr int KS_ = (KSW_) / (NW_);                                                                   \
         constexpr int NL_ = HALF_ ? KS_ / 2 : KS_;                                                            \
-        if (M <= 2 && gf_xr2())                                                                               \
+        if (M <= 2)                                                                               \
             hipLaunchKernelGGL((k_gemv_f<MODE_, LN_, NTW_, HALF_, NW_, KS_, (NL_ < ZK_GF_PF2 ? NL_ : ZK_GF_PF2),  \
                                           0, 2>),                                                             \
                                dim3(grid), dim3(64 * (NW_)), 0, (hipStream_t)stream, (const bf16_t*)A, lda,    \

@@ -27,10 +27,6 @@ constexpr int MB_MAXGS = 8;
 constexpr int GN_MAXJ = 16;      // k_gated_norm: row elements per thread held in registers (d_inner <= 4096)
 
 ZK_DEV float silu_f(float v) { return v / (1.0f + expf(-v)); }
-template <int R_>
-ZK_DEV float row_ror_f(float v) {      // DPP rotation inside each 16-lane row
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R_, 0xF, 0xF, false));
-}
 ZK_DEV float softplus_thr(float v) { return v <= 20.0f ? log1pf(expf(v)) : v; }
 
 // sum of the split-K slabs of one in_proj column, rounded to bf16 (the GEMM output dtype)
@@ -288,10 +284,10 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
 #pragma unroll
             for (int v = 0; v < NV; ++v) {         // sum over the row's 16 lanes (DPP rotations)
                 float a = accv[v];
-                a += row_ror_f<8>(a);
-                a += row_ror_f<4>(a);
-                a += row_ror_f<2>(a);
-                a += row_ror_f<1>(a);
+                a += row_ror<8>(a);
+                a += row_ror<4>(a);
+                a += row_ror<2>(a);
+                a += row_ror<1>(a);
                 const int pv = (lw * NV + v) * 4 + (ll >> 4);
                 if ((ll & 15) == 0) {
                     const float y = round_bf(a + s_x[hh * HP + pv] * Dv[h]);
@@ -462,7 +458,8 @@ extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_in
     ZK_REQUIRE(gemm_nsplit >= 1 && gemm_nsplit <= MB_MAXGS, "zk_mamba_step: gemm_nsplit=%d", gemm_nsplit);
     ZK_REQUIRE(nheads * headdim == d_inner, "zk_mamba_step: nheads*headdim != d_inner");
     bool handled = false;
-    // grouped kernel: 8 heads per workgroup (B/C conv once per group), in_proj splits 1 / 2 / 4
+    // grouped kernel: ZK_MB_HG heads per workgroup (default 1, the fastest measured; B/C conv once per
+    // group), in_proj splits 1 / 2 / 4
     const char* ge = getenv("ZK_MAMBA_GROUPED");   // "0": per-head kernel (A/B knob; read per launch call,
     const bool grouped = !(ge && ge[0] == '0');    // graph replays do not call here)
     if (grouped && nheads % ZK_MB_HG == 0 && (gemm_nsplit == 1 || gemm_nsplit == 2 || gemm_nsplit == 4)) {

@@ -46,3 +46,60 @@ def gather_codes(codes: list, device=None, group=None) -> list:
         for i in range(int(ns[r])):
             out.append(bufs[r][i, :, : int(lbs[r][i])].to(torch.int64))
     return out
+
+
+def _split_rows(cond: torch.Tensor, global_batch: int, row_base: int, local: int) -> torch.Tensor:
+    """This rank's CFG rows of a global [2B, Lc, D] conditioning: cond rows [rb, rb+n) and their
+    uncond partners [B+rb, B+rb+n) (model.py:113, 213-218 keep each pair B rows apart)."""
+    return torch.cat([cond[row_base:row_base + local], cond[global_batch + row_base:global_batch + row_base + local]])
+
+
+def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_codes: torch.Tensor | None = None,
+                     max_new_tokens: int = 86 * 30, cfg_scale: float = 2.0, batch_size: int = 1,
+                     sampling_params: dict | None = None, *, seed: int | None = None, group=None,
+                     gather: bool = True, local_input: bool = False, coll_device=None, return_local: bool = False,
+                     **generate_kw):
+    """Zonos.generate (model.py:224-457) of a GLOBAL batch of ``batch_size`` utterances sharded over
+    the ranks of ``group`` (one process per GPU) -- the library form of zonos_batch_cli.py:113-162's
+    batching with the batch split across the node's GPUs.
+
+    * Each rank takes a contiguous block of utterances (`shard`); ``row_base`` = the block's global
+      index keys the sampling noise, so each utterance's codes do not depend on the rank count
+      (within one GEMM regime).
+    * ``prefix_conditioning`` is the global [2B, Lc, D] tensor (and ``audio_prefix_codes`` the
+      global [B, 9, P]); with ``local_input=True`` they already hold only this rank's rows
+      ([2b, Lc, D] / [b, 9, P], b = the rank's share).
+    * ``seed`` None draws one seed on rank 0 from torch's generator and broadcasts it.
+    * No collective touches the decode; with ``gather`` one all_gather of the int32 codes returns
+      the global list (utterance order) on every rank, else the rank's own list;
+      ``return_local`` returns (the rank's own list on its device, the gathered list).
+    ``model`` is a ``zonos_amd.model.Zonos`` or an engine (``HipDecoder`` / ``HybridDecoder``);
+    extra keywords go to its ``generate``. Without an initialised process group this is
+    ``model.generate`` on the whole batch."""
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank(group) if world > 1 else 0
+    row_base, local = shard(batch_size, world, rank)
+    if world > 1 and seed is None:
+        s = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64) if rank == 0 else torch.zeros(1, dtype=torch.int64)
+        s = s.to(coll_device or "cpu")
+        dist.broadcast(s, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        seed = int(s.item())
+    elif seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    cond, prefix = prefix_conditioning, audio_prefix_codes
+    if not local_input and world > 1:
+        if cond.shape[0] != 2 * batch_size:
+            raise ValueError(f"Batch size mismatch: {batch_size} * 2 != {cond.shape[0]}")
+        cond = _split_rows(cond, batch_size, row_base, local)
+        if prefix is not None:
+            prefix = prefix[row_base:row_base + local]
+    if local == 0:
+        codes = []
+    else:
+        codes = model.generate(cond, prefix, max_new_tokens, cfg_scale, local, sampling_params, seed=seed,
+                               row_base=row_base, **generate_kw)
+    if world == 1 or not gather:
+        allc = codes
+    else:
+        allc = gather_codes(codes, device=coll_device, group=group)
+    return (codes, allc) if return_local else allc

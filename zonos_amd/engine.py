@@ -18,13 +18,14 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import logging
 import math
-import os
 from dataclasses import dataclass
 
 import torch
 
 from . import _lib
+from . import sampling as zsampling
 from ._lib import GenState, SamplingParams, call, ptr
 
 EOS, MASK, UNKNOWN = 1024, 1025, -1
@@ -83,12 +84,6 @@ def _split_for(N: int, K: int, M: int, target_blocks: int = 256) -> int:
     return s
 
 
-def _split_overrides() -> dict:
-    """Tuning knob (not used by default): ZK_SPLITS="qkv=4,o=4,fc2=4" fixes split-K counts."""
-    env = os.environ.get("ZK_SPLITS", "")
-    return {k: int(v) for k, v in (kv.split("=") for kv in env.split(",") if kv)}
-
-
 def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> int:
     """Workgroups per (row, kv head) for flash-decoding. Measured at R=128 (B=64): one
     workgroup per (row, kv head) (512 workgroups, no combine pass) reads 5.4-5.7 TB/s at
@@ -96,8 +91,6 @@ def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> in
     each split must cover >= 2048 keys of the cache: the combine launch costs ~6 us, more than
     it saves below that (B=1, 10 s: 1.294 ms per decode step unsplit vs 1.353 with 10 splits,
     tools/c2_attn_ab.sh)."""
-    if os.environ.get("ZK_ATTN_SPLITS"):          # tuning knob (not used by default)
-        return max(1, min(int(os.environ["ZK_ATTN_SPLITS"]), smax // 128))
     want = -(-target_blocks // (R * Hkv))
     cap = max(1, -(-smax // 2048))
     return max(1, min(want, cap, smax // 128))
@@ -109,11 +102,7 @@ def attn_merge_for(R: int, smax: int) -> int:
     small KV cache without a combine launch or in-launch tickets. 0 = unsplit attention."""
     if R > 2:
         return 0
-    env = os.environ.get("ZK_ATTN_MERGE")          # tuning knob
-    if env is None and os.environ.get("ZK_ATTN_SPLITS"):
-        return 0                                    # an explicit split count selects the other forms
-    n = int(env) if env else ATTN_MERGE_DEFAULT
-    n = min(n, smax // 128)
+    n = min(ATTN_MERGE_DEFAULT, smax // 128)
     for v in (8, 4, 2):
         if n >= v:
             return v
@@ -243,13 +232,8 @@ class HipDecoder(HipBackbone):
     """Owns device weights in engine layout and runs generate() on the GPU."""
 
     # B <= 8 decode (R <= 16 rows) runs each block as five launches (zk_gemv_fused: LayerNorm
-    # prologues, residual epilogues, no split-K slabs) instead of seven; ZK_SMALL=0 disables it
-    small_batch_path = os.environ.get("ZK_SMALL", "1") != "0"
-    # B <= 2 (R <= 4 rows) at the Zonos-v0.1-transformer geometry: the whole step's backbone +
-    # heads as ONE persistent launch (zk_decode_small, csrc/step_small.hip), bit-identical to the
-    # five-launch-per-block sequence (with ZK_GF_LAYOUT=1). Opt-in (ZK_PERSIST=1): measured 2.4x
-    # SLOWER than the launches (2.85 vs 1.20 ms per c2 step; DESIGN.md §6, profiles/r2_s3_step_small_*)
-    persistent_small = os.environ.get("ZK_PERSIST", "0") == "1"
+    # prologues, residual epilogues, no split-K slabs) instead of seven
+    small_batch_path = True
 
     def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
         super().__init__(cfg, weights, device)
@@ -286,8 +270,6 @@ class HipDecoder(HipBackbone):
             ws = self._ws
             ws["kv"].zero_()
             ws["attn_cnt"].zero_()
-            if "small" in ws:
-                ws["small"]["sync"].zero_()
             return ws
         self.release()
         D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
@@ -301,7 +283,6 @@ class HipDecoder(HipBackbone):
         # the fp32 slabs it writes and k_resid_ln reads (4.2 vs 8.4 MB; resid_ln 4.3 vs 4.8 us)
         splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R, target_blocks=128),
                       fc2=_split_for(D, Fd, R), heads=1)
-        splits.update(_split_overrides())
         part_n = max(Mp * Nqkv, Mp * D, splits["qkv"] * R * Nqkv, splits["o"] * R * D, splits["fc2"] * R * D,
                      splits["heads"] * R * Nh)
         attn_splits = attn_splits_for(R, Hk, smax)
@@ -325,54 +306,8 @@ class HipDecoder(HipBackbone):
             dbg=torch.empty(B, N_CB, VOCAB, dtype=f32, device=dev),
             graph=None,
         )
-        if self._persist(R):
-            ws["small"] = self._small_ws(ws, R)
         self._ws = ws
         return ws
-
-    def _persist(self, R: int) -> bool:
-        c = self.cfg
-        return (self.persistent_small and R <= 4 and c.d_model == 2048 and c.n_heads == 16 and c.n_kv == 4
-                and c.head_dim == 128 and c.d_ff == 8192 and self.rope_neox == 0)
-
-    def _small_ws(self, ws, R: int) -> dict:
-        """Buffers + device layer table of the persistent small-batch step (zk_decode_small)."""
-        c = self.cfg
-        dev = self.device
-        f32, bf = torch.float32, torch.bfloat16
-        D, Fd, Nqkv = c.d_model, c.d_ff, (c.n_heads + 2 * c.n_kv) * c.head_dim
-        nh = N_CB * VOCAB
-        # attention key splits (merged inside the launch): enough units to spread the KV stream of
-        # the R x 4 (row, kv head) pairs over ~64 CUs; ZK_ATTN_SPLITS pins it (same knob as the launch path)
-        env = os.environ.get("ZK_ATTN_SPLITS")
-        nsp = max(1, min(ws["smax"] // 128, int(env) if env else 64 // (R * c.n_kv)))
-        table = []
-        for i, L in enumerate(self.layers):
-            kc, vt = self._kv(ws, i)
-            table.append([ptr(L["wqkv"]), ptr(L["wo"]), ptr(L["fc1"]), ptr(L["fc2"]), ptr(L["ln1_w"]), ptr(L["ln1_b"]),
-                          ptr(L["ln2_w"]), ptr(L["ln2_b"]), ptr(kc), ptr(vt)])
-        sw = dict(
-            layers=torch.tensor(table, dtype=torch.int64, device=dev),
-            xm=torch.empty(R, D, dtype=bf, device=dev), p_qkv=torch.empty(4, R, Nqkv, dtype=f32, device=dev),
-            p_o=torch.empty(4, R, D, dtype=f32, device=dev), p_f=torch.empty(4, R, D, dtype=f32, device=dev),
-            p_heads=torch.empty(4, R, nh, dtype=f32, device=dev),
-            sync=torch.zeros(_lib.load().zk_small_sync_words(c.n_layer), dtype=torch.int32, device=dev),
-            attn_work=torch.empty(R * c.n_kv * nsp * (8 + 4 * c.head_dim), dtype=f32, device=dev),
-        )
-        scal = ws["scal"]
-        sw["args"] = _lib.SmallArgs(
-            ptr(sw["layers"]), c.n_layer, R, ws["smax"], nh, ptr(self.heads), ptr(self.lnf_w), ptr(self.lnf_b),
-            c.eps, ptr(self.freqs), ptr(scal[1:2]), ptr(ws["x"]), ptr(sw["xm"]), ptr(sw["p_qkv"]), ptr(ws["y"]),
-            ptr(sw["p_o"]), ptr(ws["h"]), ptr(sw["p_f"]), ptr(sw["p_heads"]), ptr(sw["sync"]), ptr(scal[3:4]),
-            nsp, ptr(sw["attn_work"]), None)
-        return sw
-
-    def _check_small(self, ws):
-        """A dependency wait inside zk_decode_small that gave up leaves a code in sync[32]."""
-        if "small" in ws:
-            err = int(ws["small"]["sync"][32].item())
-            if err:
-                raise _lib.ZonosHipError(f"zk_decode_small: dependency wait gave up (code {err:#x})")
 
     def release(self):
         if self._ws is not None and self._ws.get("graph"):
@@ -397,9 +332,9 @@ class HipDecoder(HipBackbone):
                         ptr(ws["stopping"]), ptr(ws["act"]), ptr(ws["rp"]), ptr(ws["tok0"]), ptr(ws["tok1"]),
                         ptr(ws["delayed"]), B, N_CB, ws["Ld"], VOCAB, seed & 0xFFFFFFFFFFFFFFFF, row_base)
 
-    # the step's launch sequence is enqueued by the C ABI (zk_decode_step); ZK_C_STEP=0 runs the
-    # same sequence from Python (bit-identical; kept as the reference for the test)
-    c_step = os.environ.get("ZK_C_STEP", "1") != "0"
+    # the step's launch sequence is enqueued by the C ABI (zk_decode_step); False runs the same
+    # sequence from Python (bit-identical; kept as the reference for the test)
+    c_step = True
 
     def _step_desc(self, ws, B, st, sp):
         """zk_step_desc of this workspace: per-layer weights + KV caches, buffers, state, params."""
@@ -422,22 +357,18 @@ class HipDecoder(HipBackbone):
     def _decode_step(self, ws, B, st, sp, stream):
         c = self.cfg
         R = 2 * B
-        if self.c_step and "small" not in ws:
+        if self.c_step:
             call("zk_decode_step", C.byref(self._step_desc(ws, B, st, sp)), stream)
             return
         scal = ws["scal"]
         skip = ptr(scal[3:4])
         L0 = self.layers[0]
-        small = self._small(R) or "small" in ws      # layer 0's LayerNorm runs in the in_proj prologue
+        small = self._small(R)                       # layer 0's LayerNorm runs in the in_proj prologue
         call("zk_embed_codes", ptr(ws["delayed"]), B, 1, N_CB, ws["Ld"] * N_CB, ws["Ld"], ptr(scal[0:1]), -1,
              ptr(self.emb), VOCAB, c.d_model, 2, ptr(ws["x"]), 1, 0, None if small else ptr(L0["ln1_w"]),
              None if small else ptr(L0["ln1_b"]), c.eps, None if small else ptr(ws["xn"]), skip, stream)
         logits, nsp = ws["part"], ws["splits"]["heads"]
-        if "small" in ws:
-            # backbone + norm_f + heads in one persistent launch; heads as 4 K-quarter slabs
-            call("zk_decode_small", C_ref(ws["small"]["args"]), stream)
-            logits, nsp = ws["small"]["p_heads"], 4
-        elif self._small(R):
+        if small:
             self._layers_small(ws, R, stream, skip)
             # heads with the final LayerNorm (norm_f) as the GEMV prologue: one fp32 slab
             call("zk_gemv_fused", ptr(ws["x"]), c.d_model, ptr(self.heads), R, N_CB * VOCAB, c.d_model, 0,
@@ -467,6 +398,10 @@ class HipDecoder(HipBackbone):
         if batch_size * 2 != prefix_conditioning.shape[0]:                            # model.py:249-250
             raise ValueError(f"Batch size mismatch: {batch_size} * 2 != {prefix_conditioning.shape[0]}")
         _lib.require_gpu(prefix_conditioning, "prefix_conditioning")
+        if prefix_conditioning.dim() != 3 or prefix_conditioning.shape[2] != self.cfg.d_model:
+            # zk_prefill copies rows of Lc * d_model bf16: a wrong width would read out of bounds
+            raise ValueError(f"prefix_conditioning must be [2B, Lc, {self.cfg.d_model}], "
+                             f"got {tuple(prefix_conditioning.shape)}")
         spd = dict(top_p=0, top_k=0, min_p=0, linear=0.55, conf=0.4, quad=0.0, repetition_penalty=3.0,
                    repetition_penalty_window=2, temperature=1.0)
         spd.update(sampling_params or {})
@@ -511,6 +446,10 @@ class HipDecoder(HipBackbone):
             call("zk_eos_step", C_ref(st), 1, P + 1, stream)
         if _after_prefill is not None:      # test hook (teacher forcing of the first frame)
             _after_prefill(ws["delayed"][..., P + 1:P + 2])
+        logdbg = zsampling.debug_enabled() or logging.getLogger().isEnabledFor(logging.DEBUG)
+        if zsampling.debug_enabled():       # the reference's sampler statistics (sampling.py:287-322)
+            zsampling.log_sampling_stats(
+                zsampling.engine_logits_row(ws["dbg"][0, 0], True, False, EOS, force_full_length), spd, None, 1.0, EOS)
         if trace is not None:
             trace.setdefault("logits", []).append(ws["dbg"].clone())
             trace.setdefault("tokens", []).append(ws["tok0"].view(B, N_CB, 1).long().clone())
@@ -526,7 +465,7 @@ class HipDecoder(HipBackbone):
         ws["rp"].fill_(float(spd["repetition_penalty"]))
 
         # ---- decode loop (model.py:345-432)
-        per_poll = 1 if (callback is not None or trace is not None) else max(1, poll_every)
+        per_poll = 1 if (callback is not None or trace is not None or logdbg) else max(1, poll_every)
         graph = None
         if use_graph and trace is None:
             graph = self._capture(ws, B, st, sp, stream)
@@ -535,12 +474,16 @@ class HipDecoder(HipBackbone):
             n = min(per_poll, max_steps - done_steps)
             if n <= 0:
                 break
+            if logdbg:                      # state the step starts from (debug logging only)
+                pre = (ws["scal"].cpu(), ws["act"][0].item(), ws["rp"][0].item(), ws["eos_mode"].cpu())
             if graph is not None:
                 call("zk_graph_launch", graph, n, stream)
             else:
                 for _ in range(n):
                     self._decode_step(ws, B, st, sp, stream)
             done_steps += n
+            if logdbg:
+                self._log_step(ws, spd, pre, force_full_length)
             if trace is not None:
                 trace["logits"].append(ws["dbg"].clone())
             scal = ws["scal"].cpu()
@@ -556,12 +499,35 @@ class HipDecoder(HipBackbone):
                 trace["tokens"].append(ws["delayed"][..., off:off + 1].clone())
             if int(scal[3]):
                 break
-        self._check_small(ws)
         offset = int(ws["scal"][0].item()) - 1
         if trace is not None:
             trace["delayed"] = ws["delayed"].clone()
             trace["offset"] = offset
         return finalize(ws["delayed"], offset, P, stream)
+
+    def _log_step(self, ws, spd, pre, force_full_length):
+        """Debug logging of one executed decode step (per_poll = 1): the sampler statistics of
+        utterance 0 / codebook 0 on the zonos.sampling loggers and model.py:381's EOS message."""
+        scal0, act0, rp0, eos0 = pre
+        off = int(scal0[0])                 # the reference's `offset` of this step
+        if int(scal0[3]):
+            return                          # generation had finished: the step was a no-op
+        scal1 = ws["scal"].cpu()
+        resampled = int(scal1[4]) > int(scal0[4])
+        if resampled:
+            eos1 = ws["eos_mode"].cpu()
+            rows = ((eos1 != 0) & (eos0 == 0)).nonzero(as_tuple=True)[0].tolist()
+            logging.debug(f"Detected EOS in codebook 0 for samples: {rows} at offset {off}. "
+                          "Resampling with -torch.inf.")
+        if not zsampling.debug_enabled():
+            return
+        x = zsampling.engine_logits_row(ws["dbg"][0, 0], False, bool(act0), EOS, force_full_length)
+        gen = ws["delayed"][0, 0, :off]
+        zsampling.log_sampling_stats(x, spd, gen, rp0, EOS)
+        if resampled:                       # the second sample_from_logits call (model.py:388)
+            if int(ws["eos_mode"][0].item()) and not int(eos0[0]):
+                x[EOS] = -math.inf
+            zsampling.log_sampling_stats(x, spd, gen, rp0, EOS)
 
     def last_logits(self) -> torch.Tensor:
         """fp32 CFG logits (before bias) of the last executed step [B][9][1026] (test hook)."""

@@ -26,7 +26,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr
-from .engine import ATTN_CHUNK, N_CB, VOCAB, HipDecoder, _split_for, _split_overrides, attn_splits_for, pack_weights
+from .engine import ATTN_CHUNK, N_CB, VOCAB, HipDecoder, _split_for, attn_splits_for, pack_weights
 
 
 @dataclass
@@ -183,7 +183,6 @@ class HybridDecoder(HipDecoder):
         # (attention out_proj 4-way and the heads unsplit, as the transformer engine: 4.645 vs 4.670 ms)
         splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R, target_blocks=128),
                       fc2=_split_for(D, max(Fd, 64), R), heads=1, inp=1, out=_split_for(D, di, R))
-        splits.update(_split_overrides())
         part_n = max(Mp * Nqkv, Mp * D, Mp * nin, splits["qkv"] * R * Nqkv, splits["o"] * R * D,
                      splits["fc2"] * R * D, splits["heads"] * R * Nh, splits["inp"] * R * nin, splits["out"] * R * D)
         attn_splits = attn_splits_for(R, Hk, smax)
@@ -226,7 +225,6 @@ class HybridDecoder(HipDecoder):
         x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
         scal = ws["scal"]
         pos_dev = None if prefill else ptr(scal[1:2])
-        inplace = os.environ.get("ZK_SSM_INPLACE") == "1"
         for i, L in enumerate(self.layers):
             if i + 1 < len(self.layers):
                 nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
@@ -255,9 +253,9 @@ class HybridDecoder(HipDecoder):
             else:
                 j = self.mamba_ids.index(i)
                 conv, ssm = ws["conv"][j], ws["ssm"][j]
-                # SSM state double-buffered by position parity (ZK_SSM_INPLACE=1: A/B knob, in place)
-                sr = 0 if inplace else S & 1
-                ssm_b = None if inplace else ptr(ssm[1])
+                # SSM state double-buffered by position parity
+                sr = S & 1
+                ssm_b = ptr(ssm[1])
                 call("zk_gemm_bf16", ptr(xn), D, ptr(L["w_in"]), M, nin, D, sp["inp"], 0, ptr(part), None, skip,
                      stream)
                 if prefill:
