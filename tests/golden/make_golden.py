@@ -322,8 +322,9 @@ def make_full_fixtures(which=("c1", "c2", "c3")):
     for name in which:
         c = FULL_CASES[name]
         B, Lc, P, T = c["B"], c["Lc"], c["P"], c["T"]
-        cond = zonos_ref.synthetic_conditioning(B, Lc, FULL.d_model, seed=1)
-        prefix = zonos_ref.synthetic_prefix_codes(B, P, seed=3) if P else None
+        cond = zonos_ref.synthetic_conditioning(B, Lc, FULL.d_model, seed=c.get("cond_seed", 1))
+        prefix = zonos_ref.synthetic_prefix_codes(B, P, seed=c.get("prefix_seed", 3)) if P else None
+        rb = c.get("row_base", 0)
         W = full_weights("copy" if name == "c1" else "random")
         model = build_ref_model(FULL, {k: (v[:1025] if k.startswith("heads") else v) for k, v in W.items()})
         d = dict(seed=np.int64(FULL_SEED))
@@ -339,12 +340,12 @@ def make_full_fixtures(which=("c1", "c2", "c3")):
             d.update(codes=codes, lens=lens, margins=m.astype(np.float32), logits=torch.stack(rec).numpy(),
                      delayed=trace["delayed"].numpy().astype(np.int16), offset=np.int32(trace["offset"]))
         else:
-            hist = forced_history(B, P, T, prefix)
+            hist = forced_history(B, P, c.get("hist_T", T), prefix, seed=c.get("hist_seed", 7))
             logits, toks, margins, steps = [], [], [], []
             for u in c["utts"]:
                 cu = torch.cat([cond[u:u + 1], cond[B + u:B + u + 1]])
-                r = ref_forced_steps(model, cu, hist[u:u + 1], P, c["windows"], CLI_SP, FULL_SEED, u)
-                o = zonos_ref.forced_steps(W, FULL, cu, hist[u:u + 1], P, c["windows"], CLI_SP, FULL_SEED, u)
+                r = ref_forced_steps(model, cu, hist[u:u + 1], P, c["windows"], CLI_SP, FULL_SEED, rb + u)
+                o = zonos_ref.forced_steps(W, FULL, cu, hist[u:u + 1], P, c["windows"], CLI_SP, FULL_SEED, rb + u)
                 steps = sorted(r)
                 for s in steps:
                     assert torch.equal(r[s][0], o[s][0]) and torch.equal(r[s][1], o[s][1]), (name, u, s)

@@ -45,6 +45,11 @@ FULL_CASES = {
     "c2": dict(B=1, Lc=160, P=0, T=861, windows=((0, 32), (800, 8)), utts=(0,), logit_steps=(0, 1, 31, 800, 807)),
     "c3": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 8), (1290, 8)), utts=(0, 37),
                logit_steps=(0, 1, 1290, 1291)),
+    # c4 = B=512 over 8 GPUs: the rank-7 shard (utterances 448..511 -> row_base 448, the inputs
+    # bench.py gives rank 7: conditioning seed 1+7, prefix seed 3+7), two utterances, at the first
+    # steps and at the last steps of the 30 s workload (context up to Lc + P + 1 + 2587 = 2998)
+    "c4": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 4), (2584, 4)), utts=(0, 37), row_base=448,
+               cond_seed=8, prefix_seed=10, hist_seed=14, hist_T=2590, logit_steps=(0, 1, 2584, 2587)),
 }
 FULL_SEED = 1234
 
@@ -78,11 +83,12 @@ def load_full_case(name):
     d = np.load(os.path.join(G, f"gen_full_{name}.npz"))
     c = dict(FULL_CASES[name])
     B, Lc, P = c["B"], c["Lc"], c["P"]
-    c["cond"] = zonos_ref.synthetic_conditioning(B, Lc, FULL.d_model, seed=1)
-    c["prefix"] = zonos_ref.synthetic_prefix_codes(B, P, seed=3) if P else None
+    c.setdefault("row_base", 0)
+    c["cond"] = zonos_ref.synthetic_conditioning(B, Lc, FULL.d_model, seed=c.get("cond_seed", 1))
+    c["prefix"] = zonos_ref.synthetic_prefix_codes(B, P, seed=c.get("prefix_seed", 3)) if P else None
     c.update({k: d[k] for k in d.files})
     if name != "c1":
-        c["history"] = forced_history(B, P, c["T"], c["prefix"])
+        c["history"] = forced_history(B, P, c.get("hist_T", c["T"]), c["prefix"], seed=c.get("hist_seed", 7))
     return c
 
 

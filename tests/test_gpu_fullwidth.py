@@ -9,6 +9,9 @@ heads 9x1026) of the HIP engine against golden vectors the REFERENCE produced
   the whole batch teacher-forced on a seeded synthetic history; its fp32 CFG logits and sampled
   tokens are compared with the reference's at the first steps and at a late context (c2: steps
   0-31 and 800-807, ctx 961-968; c3: steps 0-7 and 1290-1297, ctx 1701-1708, utterances 0 and 37).
+* c4 -- B=512 over 8 GPUs: one rank's shard run as that rank runs it (the rank-7 shard: B=64,
+  row_base 448 keys the sampling noise, rank 7's conditioning / prefix seeds), utterances 448 and
+  485 at steps 0-3 and at the last steps 2584-2587 (ctx 2995-2998, the longest context).
 """
 import numpy as np
 import pytest
@@ -86,11 +89,12 @@ def _forced_run(name):
         frame.copy_(hist[..., P + 1:P + 2])
 
     eng.generate(c["cond"].cuda(), None if c["prefix"] is None else c["prefix"].cuda(), c["T"], 2.0, B, CLI_SP,
-                 seed=FULL_SEED, force_full_length=True, callback=cb, _after_prefill=after_prefill)
+                 seed=FULL_SEED, row_base=int(c["row_base"]), force_full_length=True, callback=cb,
+                 _after_prefill=after_prefill)
     return c, got
 
 
-@pytest.mark.parametrize("name", ["c2", "c3"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c4"])
 def test_full_teacher_forced_logits_and_tokens(name):
     c, got = _forced_run(name)
     steps = [int(s) for s in c["steps"]]

@@ -236,3 +236,27 @@ def test_c_decode_step_equals_python_sequence(geom, B, monkeypatch):
     (ca, la), (cb, lb) = outs
     assert all(torch.equal(x, y) for x, y in zip(ca, cb))
     assert len(la) == len(lb) and all(torch.equal(x, y) for x, y in zip(la, lb))
+
+
+def test_sampling_loggers_do_not_change_codes(capsys):
+    """With the reference's zonos.sampling.trace logger at DEBUG (sampling.py:8, 288) generate()
+    prints the probability statistics of utterance 0 / codebook 0 every step (computed host-side
+    from the engine's logits copy) and returns exactly the codes of the silent graph run."""
+    import logging
+
+    from zonos_amd import sampling as zs
+    c = load_gen_case("sampled_cli")
+    eng = _engine(c["W"], c["cfg"])
+    args = (c["cond"].cuda(), c["prefix"].cuda(), c["max_new"], 2.0, c["B"], c["sp"])
+    quiet = eng.generate(*args, seed=c["seed"])
+    capsys.readouterr()
+    zs.trace_logger.setLevel(logging.DEBUG)
+    try:
+        loud = eng.generate(*args, seed=c["seed"])
+    finally:
+        zs.trace_logger.setLevel(logging.INFO)
+    out = capsys.readouterr().out.splitlines()
+    assert all(torch.equal(a, b) for a, b in zip(quiet, loud)) and len(quiet) == len(loud)
+    before = [l for l in out if l.startswith("Before Batch 0, Codebook 0 | Top 5:")]
+    after = [l for l in out if l.startswith("After  Batch 0, Codebook 0 | Top 5:")]
+    assert len(before) == len(after) >= c["max_new"], (len(before), out[:3])
