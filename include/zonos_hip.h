@@ -114,18 +114,6 @@ int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, i
  * K = 2048 (16 heads x 128), nsplit in {2, 4, 8}. */
 int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const void* W, int M, int N, int K,
                      void* x, const int32_t* skip, void* stream);
-/* Decode GEMM for 16 < M <= 128 on an activation in the MFMA A-operand order ("apack": element
- * (m, k) at ((k/32 * MT + m/16) * 64 + m%16 + 16 * ((k%32)/8)) * 8 + k%8, MT = ceil(M/16); rows
- * >= M zero): nn.Linear (_torch.py:114-115, 147-148) with W fragment-packed (zk_pack_weights).
- * The workgroup's waves split its K slice and stream weights and activation fragments straight
- * into registers; partial tiles are summed in a fixed order (results depend on N, K, nsplit only).
- * mode 0: fp32 split-K slabs Cpart[nsplit][M][N]; mode 1 (nsplit 1): fc1 + SwiGLU, Cout = h bf16
- * in apack order ([M] x [N/2], the fc2 input). cfg: tile configuration (0 = default). */
-int zk_gemm_apack(const void* Ap, const void* W, int M, int N, int K, int nsplit, int mode, float* Cpart,
-                  void* Cout, const int32_t* skip, int cfg, void* stream);
-/* Row-major bf16 A [M][lda] <-> apack (M <= 128, K % 32 == 0); pack zero-fills rows M..16*MT-1. */
-int zk_pack_act(const void* A, long lda, int M, int K, void* Ap, void* stream);
-int zk_unpack_act(const void* Ap, int M, int K, void* A, long lda, void* stream);
 /* fc1 weight [2F][D] (rows: F "y" then F "gate") -> interleaved groups of 8 y + 8 gate rows. */
 int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream);
 /* nn.Linear weight [N][K] bf16 -> fragment-packed [ceil64(N)/16][K/32][64][8] (rows >= N zero):

@@ -295,76 +295,6 @@ def dac():
             print(f"dac {prec:6s} B={B} T={T}: {us/1e3:8.1f} ms  {fl / (us * 1e-6) / 1e12:7.1f} TFLOP/s", flush=True)
 
 
-def ks():
-    """Decode GEMMs at the c3 shapes (M = 128): k_gemm_ws (zk_gemm_bf16, the LDS form) against
-    zk_gemm_apack (K-split waves on an apack activation) over tile configurations and split-K
-    counts; each apack configuration is first checked against torch fp32 (max |err| / max |ref|)."""
-    M = int(os.environ.get("ZK_MB_M", "128"))
-    from zonos_amd.engine import pack_weights
-    shapes = (("qkv", 3072, 2048, 0, (2, 4, 8)), ("o", 2048, 2048, 0, (4, 8, 16)), ("fc1", 16384, 2048, 1, (1,)),
-              ("fc2", 2048, 8192, 0, (4, 8, 16)), ("heads", 9234, 2048, 0, (1,)))
-    only = os.environ.get("ZK_MB_ONLY")
-    for name, N, K, mode, splits in shapes:
-        if only and name not in only.split(","):
-            continue
-        g = torch.Generator(device="cpu").manual_seed(0)
-        Wr = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).to(dev)
-        Ar = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
-        Wpk = pack_weights(Wr, S)
-        Ap = torch.zeros(((M + 15) // 16) * 16 * K, dtype=torch.bfloat16, device=dev)
-        call("zk_pack_act", ptr(Ar), K, M, K, ptr(Ap), S)
-        ref = Ar.float() @ Wr.float().T
-        if mode == 1:
-            F = N // 2
-            # engine fc1 rows are interleaved (zk_permute_fc1 order): groups of 8 y + 8 gate
-            yi = torch.arange(N, device=dev).view(-1, 16)
-            yv, gv = ref[:, yi[:, :8].reshape(-1)], ref[:, yi[:, 8:].reshape(-1)]
-            yb, gb = yv.to(torch.bfloat16).float(), gv.to(torch.bfloat16).float()
-            ref = yb * (gb / (1 + torch.exp(-gb))).to(torch.bfloat16).float()
-        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
-        Npad = (N + 63) // 64 * 64
-        Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
-        out = torch.empty(M, max(1, N // 2), dtype=torch.bfloat16, device=dev)
-        hp = torch.empty(((M + 15) // 16) * 16 * (N // 2 if mode else 1), dtype=torch.bfloat16, device=dev)
-        gb_ = N * K * 2 / 1e9
-        ns0 = 1 if mode == 1 else _split_for(N, K, M, 256)
-        part0 = torch.empty(ns0 * M * N, device=dev)
-        it = [0]
-
-        def fws():
-            W = Ws[it[0] % ncopy]
-            it[0] += 1
-            call("zk_gemm_bf16", ptr(Ar), K, ptr(W), M, N, K, ns0, mode, ptr(part0), ptr(out), None, S)
-        us = timeit(fws)
-        print(f"ks {name:5s} ws    split={ns0:2d}          : {us:7.2f} us {gb_ / (us * 1e-6):6.0f} GB/s", flush=True)
-        for ns in splits:
-            part = torch.empty(ns * M * N, device=dev)
-            for cfg in (0, 1, 2, 3):
-                try:
-                    call("zk_gemm_apack", ptr(Ap), ptr(Wpk), M, N, K, ns, mode, ptr(part), ptr(hp), None, cfg, S)
-                except Exception as e:       # no instantiation for this (split, cfg)
-                    print(f"ks {name:5s} apack split={ns:2d} cfg={cfg}: n/a ({str(e)[:60]})", flush=True)
-                    continue
-                torch.cuda.synchronize()
-                if mode == 0:
-                    got = part.view(ns, M, N).sum(0)
-                else:
-                    got = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
-                    call("zk_unpack_act", ptr(hp), M, N // 2, ptr(got), N // 2, S)
-                    got = got.float()
-                err = float((got - ref).abs().max() / ref.abs().max())
-
-                def fks():
-                    W = Ws[it[0] % ncopy]
-                    it[0] += 1
-                    call("zk_gemm_apack", ptr(Ap), ptr(W), M, N, K, ns, mode, ptr(part), ptr(hp), None, cfg, S)
-                us = timeit(fks)
-                print(f"ks {name:5s} apack split={ns:2d} cfg={cfg}: {us:7.2f} us {gb_ / (us * 1e-6):6.0f} GB/s  "
-                      f"rel err {err:.2e}", flush=True)
-            del part
-        del Ws
-
-
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("gemm", "all"):
@@ -383,5 +313,3 @@ if __name__ == "__main__":
         attn()
     if what in ("dac", "all"):
         dac()
-    if what in ("ks",):
-        ks()

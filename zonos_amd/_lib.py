@@ -79,9 +79,6 @@ _SIGS = {
     "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, I, P, P],
     "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
     "zk_gemv_fused": [P, L, P, I, I, I, I, P, P, F, P, P, P, P],
-    "zk_gemm_apack": [P, P, I, I, I, I, I, P, P, P, I, P],
-    "zk_pack_act": [P, L, I, I, P, P],
-    "zk_unpack_act": [P, I, I, P, L, P],
     "zk_permute_fc1": [P, I, I, P, P],
     "zk_pack_weights": [P, I, I, P, P],
     "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, I, P, P],

@@ -49,10 +49,11 @@ ZK_DEV size_t apack_off(int m, int k, int MT) {
     return ((size_t)((k >> 5) * MT + (m >> 4)) * 64 + (m & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
 }
 
-template <int MODE, int MT, int NC, int NW, int KS, int PF>
+// DBG (diagnostic instantiations of the sweep tool only): 1 = no activation loads, 2 = no weight loads
+template <int MODE, int MT, int NC, int NW, int KS, int PF, int DBG = 0>
 __global__ __launch_bounds__(64 * NW, 1) void k_gemm_ks(const bf16_t* __restrict__ Ap, const bf16_t* __restrict__ W,
                                                         int M, int N, int K, int kslice, float* __restrict__ Cpart,
-                                                        bf16_t* __restrict__ Cout, const int32_t* skip) {
+                                                        bf16_t* __restrict__ Cout, const int32_t* skip, int rot) {
     constexpr int ROWS = MT * 16, COLS = NC * 16;
     constexpr int RS = COLS + 4;                       // LDS row stride (floats) of a partial tile
     extern __shared__ __attribute__((aligned(16))) float red[];   // [min(NW, 4)][ROWS][RS]
@@ -69,7 +70,13 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemm_ks(const bf16_t* __restrict
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ln = lane & 15, lg = lane >> 4;
     const int n0 = bx * COLS, split = bz;
-    const int ks0 = (split * kslice >> 5) + w * KS;    // first k-step of this wave
+    // rot 1: the waves' K ranges rotate with the tile (wave w takes range (w + bx) % NW; the partial
+    // tiles are summed in range order, so the result is the same); rot 2: also each wave starts its
+    // range at k-step bx % KS (changes the accumulation order per tile). Both spread the 256
+    // workgroups' reads of the shared activation over the L2 instead of marching in lockstep.
+    const int wr_ = rot ? (w + bx) % NW : w;
+    const int r0 = rot == 2 ? bx % KS : 0;
+    const int ks0 = (split * kslice >> 5) + wr_ * KS;  // first k-step of this wave's range
     const int KT = K >> 5;
     const bf16_t* wp[NC];
 #pragma unroll
@@ -84,10 +91,11 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemm_ks(const bf16_t* __restrict
     constexpr int U = PF + 1;
     uint4 wr[U][NC], ar[U][MT];
     auto issue = [&](int s, int slot) {
+        const int sa = (s + r0) & (KS - 1);
 #pragma unroll
-        for (int t = 0; t < NC; ++t) wr[slot][t] = ldg_nt(wp[t] + s * 512);
+        for (int t = 0; t < NC; ++t) wr[slot][t] = (DBG & 2) ? make_uint4(sa, t, lane, 0) : ldg_nt(wp[t] + sa * 512);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) ar[slot][m] = ldg(ap + ((size_t)s * MT + m) * 512);
+        for (int m = 0; m < MT; ++m) ar[slot][m] = (DBG & 1) ? make_uint4(sa, m, lane, 1) : ldg(ap + ((size_t)sa * MT + m) * 512);
     };
 #pragma unroll
     for (int p = 0; p < PF; ++p)
@@ -108,7 +116,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemm_ks(const bf16_t* __restrict
     // held at once: with NW = 8 waves w >= 4 hand theirs to wave w - 4 first, so the fixed summation
     // order is (w0 + w4) + (w1 + w5) + (w2 + w6) + (w3 + w7).
     constexpr int NWL = NW > 4 ? 4 : NW;
-    float* mine = red + (size_t)(w % NWL) * ROWS * RS;
+    float* mine = red + (size_t)(wr_ % NWL) * ROWS * RS;
     auto tile_io = [&](bool store) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
@@ -122,12 +130,12 @@ __global__ __launch_bounds__(64 * NW, 1) void k_gemm_ks(const bf16_t* __restrict
                 }
     };
     if constexpr (NW > 4) {
-        if (w >= 4) tile_io(true);
+        if (wr_ >= 4) tile_io(true);
         __syncthreads();
-        if (w < 4) tile_io(false);
+        if (wr_ < 4) tile_io(false);
         __syncthreads();
     }
-    if (w < NWL) tile_io(true);
+    if (wr_ < NWL) tile_io(true);
     __syncthreads();
     constexpr int NTH = 64 * NW;
     if constexpr (MODE == 0) {
@@ -199,16 +207,16 @@ __global__ void k_unpack_act(const bf16_t* __restrict__ Ap, int M, int K, int MT
     }
 }
 
-template <int MODE, int MT, int NC, int NW, int KS, int PF>
+template <int MODE, int MT, int NC, int NW, int KS, int PF, int DBG = 0>
 int launch_ks(const bf16_t* Ap, const bf16_t* W, int M, int N, int K, int nsplit, float* Cpart, bf16_t* Cout,
-              const int32_t* skip, hipStream_t st) {
+              const int32_t* skip, int rot, hipStream_t st) {
     const int tiles = (N + NC * 16 - 1) / (NC * 16);
     const size_t lds = (size_t)(NW > 4 ? 4 : NW) * MT * 16 * (NC * 16 + 4) * sizeof(float);
-    auto kern = &k_gemm_ks<MODE, MT, NC, NW, KS, PF>;
+    auto kern = &k_gemm_ks<MODE, MT, NC, NW, KS, PF, DBG>;
     if (lds > 65536) hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)lds);
     hipLaunchKernelGGL(kern, dim3(tiles, 1, nsplit), dim3(64 * NW), lds, st, Ap, W, M, N, K, K / nsplit, Cpart, Cout,
-                       skip);
+                       skip, rot);
     return 0;
 }
 
@@ -221,7 +229,8 @@ int launch_ks(const bf16_t* Ap, const bf16_t* W, int M, int N, int K, int nsplit
 //   fc2      N 2048, K 8192: 64 columns, split 8, 4 waves x 8 k-steps  -> 256 workgroups
 //   heads    N 9234, K 2048: 64 columns, split 1, 4 waves x 16 k-steps -> 145 workgroups
 // `cfg` selects (NC, NW, PF) for the sweep tool: 0 = default (NC 4, NW 4, PF 3), 1 = (4, 8, 1),
-// 2 = (2, 4, 4), 3 = (4, 4, 2).
+// 2 = (2, 4, 4), 3 = (4, 4, 2), 7 = (4, 4, 4); 4 / 5 / 6 = 3 without activation / weight / any
+// loads (diagnostics, wrong results); + 16 * rot (k_gemm_ks `rot`).
 extern "C" int zk_gemm_apack(const void* Ap, const void* W, int M, int N, int K, int nsplit, int mode, float* Cpart,
                              void* Cout, const int32_t* skip, int cfg, void* stream) {
     ZK_REQUIRE(M > 0 && M <= 128 && N > 0 && K > 0 && nsplit >= 1 && K % (32 * nsplit) == 0,
@@ -231,6 +240,8 @@ extern "C" int zk_gemm_apack(const void* Ap, const void* W, int M, int N, int K,
                "zk_gemm_apack: mode %d needs %s", mode, mode == 0 ? "Cpart" : "Cout, nsplit 1, N % 64 == 0");
     const int MT = (M + 15) / 16;
     const int steps = K / nsplit / 32;      // k-steps per workgroup
+    const int rot = cfg >> 4;               // cfg bits 4-5: K-order rotation (k_gemm_ks `rot`)
+    cfg &= 15;
     hipStream_t st = (hipStream_t)stream;
     const auto* A = (const bf16_t*)Ap;
     const auto* Wp = (const bf16_t*)W;
@@ -238,9 +249,12 @@ extern "C" int zk_gemm_apack(const void* Ap, const void* W, int M, int N, int K,
     int rc = -1;
 #define ZK_KS_MT(MODE_, NC_, NW_, KS_, PF_)                                                                         \
     switch (MT) {                                                                                                   \
-        case 8: rc = launch_ks<MODE_, 8, NC_, NW_, KS_, PF_>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, st); break;    \
-        case 4: rc = launch_ks<MODE_, 4, NC_, NW_, KS_, PF_>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, st); break;    \
-        case 2: rc = launch_ks<MODE_, 2, NC_, NW_, KS_, PF_>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, st); break;    \
+        case 8: rc = cfg == 4 ? launch_ks<MODE_, 8, NC_, NW_, KS_, PF_, 1>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, rot, st) \
+                   : cfg == 5 ? launch_ks<MODE_, 8, NC_, NW_, KS_, PF_, 2>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, rot, st) \
+                   : cfg == 6 ? launch_ks<MODE_, 8, NC_, NW_, KS_, PF_, 3>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, rot, st) \
+                   : launch_ks<MODE_, 8, NC_, NW_, KS_, PF_>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, rot, st); break;    \
+        case 4: rc = launch_ks<MODE_, 4, NC_, NW_, KS_, PF_>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, rot, st); break;    \
+        case 2: rc = launch_ks<MODE_, 2, NC_, NW_, KS_, PF_>(A, Wp, M, N, K, nsplit, Cpart, Cb, skip, rot, st); break;    \
         default: break;                                                                                             \
     }
 #define ZK_KS_STEPS(MODE_, NC_, NW_, PF_)                                                                           \
@@ -257,6 +271,8 @@ extern "C" int zk_gemm_apack(const void* Ap, const void* W, int M, int N, int K,
         case 1: ZK_KS_STEPS(MODE_, 4, 8, 1) break;                      \
         case 2: ZK_KS_STEPS(MODE_, 2, 4, 4) break;                      \
         case 3: ZK_KS_STEPS(MODE_, 4, 4, 2) break;                      \
+        case 4: case 5: case 6: ZK_KS_STEPS(MODE_, 4, 4, 2) break;      \
+        case 7: ZK_KS_STEPS(MODE_, 4, 4, 4) break;                      \
         default: ZK_KS_STEPS(MODE_, 4, 4, 3) break;                     \
     }
     if (mode == 0) { ZK_KS_CFG(0) } else { ZK_KS_CFG(1) }
