@@ -277,6 +277,74 @@ int zk_decode_step(const zk_step_desc* d, void* stream);
  * The loop state (st.scal, eos_mode, ...) is initialised by the host afterwards (model.py:316-342). */
 int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P, void* q, void* stream);
 
+/* ------------------------------------------------------------------ hybrid decode step
+ * The same two entries for the Zonos-v0.1-hybrid backbone (zonos/backbone/_mamba_ssm.py:9-57 ->
+ * mamba_ssm create_block: Mamba2 mixers, MHA + GatedMLP at attn_layer_idx, fused add + LayerNorm
+ * of the fp32 sum), the launch sequence of zonos_amd.hybrid.HybridDecoder:
+ *   Mamba2 layer : in_proj GEMM -> zk_mamba_step (conv + SSM state update, y * silu(z)) ->
+ *                  zk_gated_rmsnorm -> out_proj GEMM -> zk_resid_ln(ln_on_sum = 1, next norm)
+ *   attention    : Wqkv GEMM -> zk_attn_decode_qkv (GPT-NeoX RoPE) -> out_proj -> zk_resid_ln(norm2)
+ *                  -> fc1 (SwiGLU) -> fc2 -> zk_resid_ln(next norm)
+ * then norm_f, the 9 heads, the sampler and the EOS protocol exactly as zk_decode_step. Conv and
+ * SSM states are double-buffered by step parity ({a, b}, zk_mamba_step). Replaces the
+ * `_decode_one_token` / `_prefill` bodies of model.py:118-202 for the mamba_ssm backbone (the one
+ * the reference CUDA-graph-captures, model.py:220-222). */
+typedef struct zk_hybrid_layer {
+    int32_t type;           /* 0 attention block, 1 Mamba2 block */
+    int32_t pad_;
+    const void* ln1_w;      /* norm.weight / bias (bf16 [D]) */
+    const void* ln1_b;
+    /* attention block */
+    const void* wqkv;       /* mixer.in_proj, packed */
+    const void* wo;         /* mixer.out_proj, packed */
+    const void* ln2_w;      /* norm2 */
+    const void* ln2_b;
+    const void* fc1;        /* mlp.fc1 (zk_permute_fc1 order), packed */
+    const void* fc2;        /* mlp.fc2, packed */
+    void* k_cache;          /* fragment-order K / V^T caches */
+    void* vt_cache;
+    /* Mamba2 block */
+    const void* w_in;       /* mixer.in_proj, packed [2 d_inner + 2 d_state + nheads][D] */
+    const float* conv_w;    /* conv1d weight fp32 [conv_dim][4] */
+    const float* conv_b;    /* conv1d bias fp32 [conv_dim] */
+    const float* A;         /* -exp(A_log) fp32 [nheads] */
+    const float* dt_bias;   /* fp32 [nheads] */
+    const float* Dskip;     /* D fp32 [nheads] */
+    const float* norm_w;    /* RMSNormGated weight fp32 [d_inner] */
+    const void* w_out;      /* mixer.out_proj, packed [D][d_inner] */
+    void* conv_state[2];    /* bf16 [R][conv_dim][4], parity buffers */
+    void* ssm_state[2];     /* bf16 [R][nheads][headdim][d_state], parity buffers */
+} zk_hybrid_layer;
+
+typedef struct zk_hybrid_desc {
+    int32_t B, n_layer, d_model, n_heads, n_kv, head_dim, d_ff, smax;
+    int32_t d_inner, nheads_ssm, headdim_ssm, d_state;
+    int32_t split_qkv, split_o, split_fc2, split_heads, split_inp, split_out, attn_splits, pad_;
+    float eps;                     /* LayerNorm eps (norm_epsilon) */
+    float gate_eps;                /* RMSNormGated eps (1e-5 in mamba_ssm Mamba2) */
+    const zk_hybrid_layer* layers; /* [n_layer] */
+    const void* emb;               /* codebook embeddings bf16 [9][1026][D] */
+    const void* heads;             /* 9 heads stacked, packed */
+    const void* lnf_w;             /* norm_f */
+    const void* lnf_b;
+    const float* freqs;            /* bf16-rounded cos/sin cache [pos][hd/2][2] (rope_neox) */
+    void* x;                       /* residual rows bf16 [rows][D] */
+    void* xn;                      /* LayerNorm'd rows bf16 */
+    void* y;                       /* attention output bf16 [rows][H*hd] */
+    void* h;                       /* SwiGLU output bf16 [rows][d_ff] */
+    float* part;                   /* split-K slabs / logits */
+    float* attn_work;              /* split-KV partials */
+    float* yz;                     /* Mamba y * silu(z) fp32 [rows][d_inner] */
+    void* ym;                      /* RMSNormGated output bf16 [rows][d_inner] */
+    void* xc;                      /* prefill conv scratch bf16 [rows][conv_dim] */
+    float* dbg;                    /* nullable: fp32 CFG logits of draw 0 */
+    zk_gen_state st;
+    zk_sampling_params sp;
+} zk_hybrid_desc;
+
+int zk_hybrid_decode_step(const zk_hybrid_desc* d, void* stream);
+int zk_hybrid_prefill(const zk_hybrid_desc* d, const void* cond, int Lc, int P, void* q, void* stream);
+
 /* ------------------------------------------------------------------ DAC decoder
  * (zonos/autoencoder.py:44-47 -> modeling_dac.py:610-640). fp32 activations, layout
  * [B][C][T] (channels-first, like torch). Per-row valid lengths (in frames) make a

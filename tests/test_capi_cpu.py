@@ -136,5 +136,7 @@ def test_ctypes_struct_layouts_match_the_c_abi(lib):
     assert lib.zk_abi_size(14) == _lib.StepDesc.st.offset and lib.zk_abi_size(15) == _lib.StepDesc.sp.offset
     assert lib.zk_abi_size(8) == C.sizeof(_lib.DacDesc) and lib.zk_abi_size(17) == C.sizeof(_lib.DacBlock)
     assert lib.zk_abi_size(16) == _lib.DacDesc.blocks.offset
+    assert lib.zk_abi_size(18) == C.sizeof(_lib.HybridLayer) and lib.zk_abi_size(19) == C.sizeof(_lib.HybridDesc)
+    assert lib.zk_abi_size(20) == _lib.HybridDesc.st.offset and lib.zk_abi_size(21) == _lib.HybridDesc.eps.offset
 
 

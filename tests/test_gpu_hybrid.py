@@ -312,3 +312,32 @@ def test_hybrid_c5_batch64_teacher_forced_logits():
         assert np.array_equal(r[clear].argmax(-1), g[clear].argmax(-1)), s
     print("hybrid c5 B=64 teacher-forced logits (max |d|, mean |d|, mean |logit|) per step:", errs)
     assert max(e[1] / e[2] for e in errs) < 0.06 and max(e[0] for e in errs) < 2.0, errs
+
+
+@pytest.mark.parametrize("geom,B", [("tiny", 3), ("full4", 12)])
+def test_c_hybrid_step_equals_python_sequence(geom, B, monkeypatch):
+    """zk_hybrid_prefill + zk_hybrid_decode_step (the hybrid prefill and decode step enqueued by the
+    C ABI, so a non-Python host can drive config c5) == the same launch sequences issued from
+    Python (HybridDecoder with c_step off): identical per-step logits and codes, eager; and the
+    hipGraph replay of the C step gives the eager codes."""
+    from zonos_amd.hybrid import HybridDecoder
+    c = TINYH if geom == "tiny" else HR.HybridCfg(n_layer=4, attn_layer_idx=(2,))
+    W = HR.make_weights(c, seed=7, head_scale=4.0)
+    eng = _engine(W, c)
+    cond = zonos_ref.synthetic_conditioning(B, 12, c.d_model, seed=2).to(DEV)
+    prefix = zonos_ref.synthetic_prefix_codes(B, 3, seed=4).to(DEV)
+    sp = dict(temperature=1.0, top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
+              repetition_penalty_window=8)
+    outs = []
+    for flag in (True, False):
+        monkeypatch.setattr(HybridDecoder, "c_step", flag)
+        eng._ws = None
+        trace = {}
+        out = eng.generate(cond, prefix, 16, 2.0, B, sp, seed=9, trace=trace)
+        outs.append(([o.cpu() for o in out], [t.cpu() for t in trace["logits"]]))
+    (ca, la), (cb, lb) = outs
+    assert all(torch.equal(x, y) for x, y in zip(ca, cb)) and len(ca) == len(cb)
+    assert len(la) == len(lb) and all(torch.equal(x, y) for x, y in zip(la, lb))
+    monkeypatch.setattr(HybridDecoder, "c_step", True)
+    g = eng.generate(cond, prefix, 16, 2.0, B, sp, seed=9, poll_every=4)          # hipGraph of the C step
+    assert all(torch.equal(x.cpu(), y) for x, y in zip(g, ca))

@@ -49,6 +49,23 @@ class StepDesc(C.Structure):
                ("st", GenState), ("sp", SamplingParams)]
 
 
+class HybridLayer(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pad_", C.c_int32), ("ln1_w", P), ("ln1_b", P), ("wqkv", P), ("wo", P),
+                ("ln2_w", P), ("ln2_b", P), ("fc1", P), ("fc2", P), ("k_cache", P), ("vt_cache", P), ("w_in", P),
+                ("conv_w", P), ("conv_b", P), ("A", P), ("dt_bias", P), ("Dskip", P), ("norm_w", P), ("w_out", P),
+                ("conv_state", P * 2), ("ssm_state", P * 2)]
+
+
+class HybridDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("B", "n_layer", "d_model", "n_heads", "n_kv", "head_dim", "d_ff", "smax",
+                                         "d_inner", "nheads_ssm", "headdim_ssm", "d_state", "split_qkv", "split_o",
+                                         "split_fc2", "split_heads", "split_inp", "split_out", "attn_splits",
+                                         "pad_")] + \
+              [("eps", F), ("gate_eps", F), ("layers", P), ("emb", P), ("heads", P), ("lnf_w", P), ("lnf_b", P),
+               ("freqs", P), ("x", P), ("xn", P), ("y", P), ("h", P), ("part", P), ("attn_work", P), ("yz", P),
+               ("ym", P), ("xc", P), ("dbg", P), ("st", GenState), ("sp", SamplingParams)]
+
+
 class DacResUnit(C.Structure):
     _fields_ = [("dil", C.c_int32), ("a1", P), ("w1", P), ("b1", P), ("a2", P), ("w2", P), ("b2", P)]
 
@@ -89,6 +106,8 @@ _SIGS = {
     "zk_gemv_attn_out": [P, I, I, P, I, I, I, P, P, P],
     "zk_decode_step": [C.POINTER(StepDesc), P],
     "zk_prefill": [C.POINTER(StepDesc), P, I, I, P, P],
+    "zk_hybrid_decode_step": [C.POINTER(HybridDesc), P],
+    "zk_hybrid_prefill": [C.POINTER(HybridDesc), P, I, I, P, P],
     "zk_dac_decode": [C.POINTER(DacDesc), P, I, I, P, P, C.c_size_t, P, P],
     "zk_mamba_step": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "zk_mamba_prefill": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P],

@@ -25,7 +25,7 @@ extern "C" int zk_version(void) { return 1; }
 
 // sizeof / offsetof of the by-value ABI structs, so a binding (ctypes here) can verify its
 // layout without a GPU: which = 0 zk_sampling_params, 1 zk_gen_state, 4 ZkCondSeg, 5 ZkCondPlan,
-// 6 zk_step_layer, 7 zk_step_desc, 8 zk_dac_desc; 12-17 field offsets (see the cases).
+// 6 zk_step_layer, 7 zk_step_desc, 8 zk_dac_desc; 12-21 sizes / field offsets (see the cases).
 extern "C" long zk_abi_size(int which) {
     switch (which) {
         case 0: return (long)sizeof(zk_sampling_params);
@@ -41,6 +41,10 @@ extern "C" long zk_abi_size(int which) {
         case 8: return (long)sizeof(zk_dac_desc);
         case 16: return (long)offsetof(zk_dac_desc, blocks);
         case 17: return (long)sizeof(zk_dac_block);
+        case 18: return (long)sizeof(zk_hybrid_layer);
+        case 19: return (long)sizeof(zk_hybrid_desc);
+        case 20: return (long)offsetof(zk_hybrid_desc, st);
+        case 21: return (long)offsetof(zk_hybrid_desc, eps);
         default: return -1;
     }
 }
@@ -73,7 +77,7 @@ extern "C" int zk_graph_end(void* stream, void** graph_exec) {
     HIPCHK(hipStreamEndCapture((hipStream_t)stream, &g), "zk_graph_end(capture)");
     hipGraphExec_t ex = nullptr;
     hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-    hipGraphDestroy(g);
+    (void)hipGraphDestroy(g);
     HIPCHK(e, "zk_graph_end(instantiate)");
     *graph_exec = (void*)ex;
     return 0;
@@ -222,6 +226,112 @@ extern "C" int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P
                             last ? d->lnf_b : d->layers[i + 1].ln1_b, d->eps, M, D, d->x, d->xn, 0, nullptr, stream));
     }
     // heads on the last position of every row (rows r*S + S-1 via lda = S*D)
+    ZK_STEP(zk_gemm_bf16(static_cast<const char*>(d->xn) + (size_t)(S - 1) * row, (long)S * D, d->heads, R, K * V, D,
+                         d->split_heads, 0, d->part, nullptr, nullptr, stream));
+    ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 1, 0, d->dbg, stream));
+    ZK_STEP(zk_eos_step(&d->st, 1, P + 1, stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------ hybrid step (zonos_amd.hybrid)
+namespace {
+bool hybrid_ok(const zk_hybrid_desc* d) {
+    return d != nullptr && d->layers != nullptr && d->n_layer > 0 && d->B > 0 && d->d_inner > 0 &&
+           d->nheads_ssm * d->headdim_ssm == d->d_inner;
+}
+
+// the block sequence of HybridDecoder._layers over M = R*S rows; prefill: S positions per row
+int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, void* stream) {
+    const int M = R * S;
+    const int D = d->d_model, H = d->n_heads, Hk = d->n_kv, hd = d->head_dim, Fd = d->d_ff;
+    const int Nqkv = (H + 2 * Hk) * hd, di = d->d_inner, nh = d->nheads_ssm;
+    const int nin = 2 * di + 2 * d->d_state + nh;
+    const int32_t* scal = d->st.scal;
+    const int32_t* skip = prefill ? nullptr : scal + 3;
+    const int32_t* pos = prefill ? nullptr : scal + 1;
+    const int sq = prefill ? 1 : d->split_qkv, so = prefill ? 1 : d->split_o, sf = prefill ? 1 : d->split_fc2;
+    const int si = prefill ? 1 : d->split_inp, su = prefill ? 1 : d->split_out;
+    for (int i = 0; i < d->n_layer; ++i) {
+        const zk_hybrid_layer& L = d->layers[i];
+        const bool last = i + 1 == d->n_layer;
+        const void* nw = last ? d->lnf_w : d->layers[i + 1].ln1_w;
+        const void* nb = last ? d->lnf_b : d->layers[i + 1].ln1_b;
+        if (L.type == 0) {
+            ZK_STEP(zk_gemm_bf16(d->xn, D, L.wqkv, M, Nqkv, D, sq, 0, d->part, nullptr, skip, stream));
+            if (prefill) {
+                ZK_STEP(zk_qkv_rope(d->part, 1, R, S, H, Hk, hd, d->freqs, 0, nullptr, q, L.k_cache, L.vt_cache,
+                                    d->smax, nullptr, 1, nullptr, stream));
+                ZK_STEP(zk_attn_prefill(q, L.k_cache, L.vt_cache, R, S, H, Hk, hd, d->smax, d->y, stream));
+            } else {
+                ZK_STEP(zk_attn_decode_qkv(d->part, sq, d->freqs, L.k_cache, L.vt_cache, R, H, Hk, hd, d->smax, 1,
+                                           pos, d->attn_work, d->attn_splits, d->y, 1, skip, stream));
+            }
+            ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, M, D, H * hd, so, 0, d->part, nullptr, skip, stream));
+            ZK_STEP(zk_resid_ln(d->part, so, d->x, L.ln2_w, L.ln2_b, d->eps, M, D, d->x, d->xn, 1, skip, stream));
+            ZK_STEP(zk_gemm_bf16(d->xn, D, L.fc1, M, 2 * Fd, D, 1, 1, nullptr, d->h, skip, stream));
+            ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, M, D, Fd, sf, 0, d->part, nullptr, skip, stream));
+            ZK_STEP(zk_resid_ln(d->part, sf, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, stream));
+        } else if (L.type == 1) {
+            ZK_STEP(zk_gemm_bf16(d->xn, D, L.w_in, M, nin, D, si, 0, d->part, nullptr, skip, stream));
+            if (prefill) {
+                // the first decode step (position S) reads the parity-(S & 1) buffers
+                ZK_STEP(zk_mamba_prefill(d->part, R, S, di, nh, d->headdim_ssm, d->d_state, L.conv_w, L.conv_b, d->xc,
+                                         L.conv_state[S & 1], L.ssm_state[S & 1], L.A, L.dt_bias, L.Dskip, d->yz,
+                                         stream));
+            } else {
+                ZK_STEP(zk_mamba_step(d->part, si, R, di, nh, d->headdim_ssm, d->d_state, L.conv_w, L.conv_b,
+                                      L.conv_state[0], L.conv_state[1], pos, L.ssm_state[0], L.ssm_state[1], L.A,
+                                      L.dt_bias, L.Dskip, d->yz, skip, stream));
+            }
+            ZK_STEP(zk_gated_rmsnorm(d->yz, M, di, L.norm_w, d->gate_eps, d->ym, skip, stream));
+            ZK_STEP(zk_gemm_bf16(d->ym, di, L.w_out, M, D, di, su, 0, d->part, nullptr, skip, stream));
+            ZK_STEP(zk_resid_ln(d->part, su, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, stream));
+        } else {
+            zk_set_error("zk_hybrid: layer %d has unknown type %d", i, L.type);
+            return -1;
+        }
+    }
+    return 0;
+}
+}  // namespace
+
+extern "C" int zk_hybrid_decode_step(const zk_hybrid_desc* d, void* stream) {
+    if (!hybrid_ok(d)) {
+        zk_set_error("zk_hybrid_decode_step: bad descriptor");
+        return -1;
+    }
+    const int K = d->st.K, V = d->st.V, B = d->B, R = 2 * B, D = d->d_model;
+    int32_t* scal = d->st.scal;
+    const int32_t* skip = scal + 3;
+    ZK_STEP(zk_embed_codes(d->st.delayed, B, 1, K, (long)d->st.Ld * K, d->st.Ld, scal, -1, d->emb, V, D, 2, d->x, 1, 0,
+                           d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, d->xn, skip, stream));
+    ZK_STEP(hybrid_layers(d, R, 1, false, nullptr, stream));
+    ZK_STEP(zk_gemm_bf16(d->xn, D, d->heads, R, K * V, D, d->split_heads, 0, d->part, nullptr, skip, stream));
+    ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 0, 0, d->dbg, stream));
+    ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 0, 1, nullptr, stream));
+    ZK_STEP(zk_eos_step(&d->st, 0, 0, stream));
+    return 0;
+}
+
+extern "C" int zk_hybrid_prefill(const zk_hybrid_desc* d, const void* cond, int Lc, int P, void* q, void* stream) {
+    if (!hybrid_ok(d) || cond == nullptr || q == nullptr || Lc < 0 || P < 0) {
+        zk_set_error("zk_hybrid_prefill: bad arguments");
+        return -1;
+    }
+    const int K = d->st.K, V = d->st.V, B = d->B, R = 2 * B, S = Lc + P + 1, D = d->d_model;
+    const size_t row = (size_t)D * 2;
+    if (Lc > 0) {
+        hipError_t e = hipMemcpy2DAsync(d->x, S * row, cond, Lc * row, Lc * row, R, hipMemcpyDeviceToDevice,
+                                        (hipStream_t)stream);
+        if (e != hipSuccess) {
+            zk_set_error("zk_hybrid_prefill: conditioning copy: %s", hipGetErrorString(e));
+            return -1;
+        }
+    }
+    ZK_STEP(zk_embed_codes(d->st.delayed, B, P + 1, K, (long)d->st.Ld * K, d->st.Ld, nullptr, 0, d->emb, V, D, 2,
+                           d->x, S, Lc, nullptr, nullptr, d->eps, nullptr, nullptr, stream));
+    ZK_STEP(zk_layernorm(d->x, d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, R * S, D, d->xn, stream));
+    ZK_STEP(hybrid_layers(d, R, S, true, q, stream));
     ZK_STEP(zk_gemm_bf16(static_cast<const char*>(d->xn) + (size_t)(S - 1) * row, (long)S * D, d->heads, R, K * V, D,
                          d->split_heads, 0, d->part, nullptr, nullptr, stream));
     ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 1, 0, d->dbg, stream));

@@ -354,11 +354,17 @@ class HipDecoder(HipBackbone):
                              ptr(self.lnf_b), ptr(self.freqs), ptr(ws["x"]), ptr(ws["xn"]), ptr(ws["y"]), ptr(ws["h"]),
                              ptr(ws["part"]), ptr(ws["attn_work"]), ptr(ws["attn_cnt"]), ptr(ws["dbg"]), st, sp)
 
+    def _c_decode(self, ws, B, st, sp, stream):
+        call("zk_decode_step", C.byref(self._step_desc(ws, B, st, sp)), stream)
+
+    def _c_prefill(self, ws, B, st, sp, cond, Lc, P, stream):
+        call("zk_prefill", C.byref(self._step_desc(ws, B, st, sp)), ptr(cond), Lc, P, ptr(ws["q"]), stream)
+
     def _decode_step(self, ws, B, st, sp, stream):
         c = self.cfg
         R = 2 * B
         if self.c_step:
-            call("zk_decode_step", C.byref(self._step_desc(ws, B, st, sp)), stream)
+            self._c_decode(ws, B, st, sp, stream)
             return
         scal = ws["scal"]
         skip = ptr(scal[3:4])
@@ -430,7 +436,7 @@ class HipDecoder(HipBackbone):
         # ---- prefill (model.py:297-319, _prefill 181-202)
         if self.c_step:        # the same sequence enqueued by the C ABI
             condb = ws["cond_keep"] = prefix_conditioning.to(torch.bfloat16).contiguous()   # alive until copied
-            call("zk_prefill", C.byref(self._step_desc(ws, B, st, sp)), ptr(condb), Lc, P, ptr(ws["q"]), stream)
+            self._c_prefill(ws, B, st, sp, condb, Lc, P, stream)
         else:
             x = ws["x"][: R * S].view(R, S, D)
             x[:, :Lc].copy_(prefix_conditioning.to(torch.bfloat16))

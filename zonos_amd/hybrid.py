@@ -18,8 +18,7 @@ Prefill runs the causal conv over the prefix and the exact recurrence (zk_mamba_
 """
 from __future__ import annotations
 
-import math
-import os
+import ctypes as C
 from dataclasses import dataclass
 
 import torch
@@ -97,7 +96,9 @@ class HybridDecoder(HipDecoder):
     """generate() for the hybrid backbone (the layer loop and state differ from HipDecoder)."""
 
     small_batch_path = False      # the hybrid block sequence has its own _layers (prenorm add + norm)
-    c_step = False                # zk_decode_step is the transformer's sequence; the hybrid's stays here
+    # the step / prefill sequences are enqueued by the C ABI (zk_hybrid_decode_step / zk_hybrid_prefill);
+    # False issues the same sequence from Python (bit-identical; the reference for the test)
+    c_step = True
 
     def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda"):
         _lib.load()
@@ -214,6 +215,45 @@ class HybridDecoder(HipDecoder):
     def _kv(self, ws, layer):
         j = self.attn_ids.index(layer)
         return ws["kv"][j, 0], ws["kv"][j, 1]
+
+    # ------------------------------------------------------------------ C ABI descriptor
+    def _step_desc(self, ws, B, st, sp):
+        """zk_hybrid_desc of this workspace: per-layer weights + states, buffers, state, params."""
+        c = self.cfg
+        if "hybrid_layers" not in ws:
+            arr = (_lib.HybridLayer * c.n_layer)()
+            for i, L in enumerate(self.layers):
+                e = _lib.HybridLayer()
+                e.ln1_w, e.ln1_b = ptr(L["ln1_w"]), ptr(L["ln1_b"])
+                if L["type"] == "attn":
+                    kc, vt = self._kv(ws, i)
+                    e.type = 0
+                    e.wqkv, e.wo, e.ln2_w, e.ln2_b = ptr(L["wqkv"]), ptr(L["wo"]), ptr(L["ln2_w"]), ptr(L["ln2_b"])
+                    e.fc1, e.fc2, e.k_cache, e.vt_cache = ptr(L["fc1"]), ptr(L["fc2"]), ptr(kc), ptr(vt)
+                else:
+                    j = self.mamba_ids.index(i)
+                    e.type = 1
+                    e.w_in, e.conv_w, e.conv_b = ptr(L["w_in"]), ptr(L["conv_w"]), ptr(L["conv_b"])
+                    e.A, e.dt_bias, e.Dskip = ptr(L["A"]), ptr(L["dt_bias"]), ptr(L["D"])
+                    e.norm_w, e.w_out = ptr(L["norm_w"]), ptr(L["w_out"])
+                    e.conv_state[0], e.conv_state[1] = ptr(ws["conv"][j][0]), ptr(ws["conv"][j][1])
+                    e.ssm_state[0], e.ssm_state[1] = ptr(ws["ssm"][j][0]), ptr(ws["ssm"][j][1])
+                arr[i] = e
+            ws["hybrid_layers"] = arr
+        sps = ws["splits"]
+        return _lib.HybridDesc(B, c.n_layer, c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff, ws["smax"],
+                               c.d_inner, c.nheads_ssm, c.headdim, c.d_state, sps["qkv"], sps["o"], sps["fc2"],
+                               sps["heads"], sps["inp"], sps["out"], ws["attn_splits"], 0, c.eps, 1e-5,
+                               C.cast(ws["hybrid_layers"], C.c_void_p), ptr(self.emb), ptr(self.heads),
+                               ptr(self.lnf_w), ptr(self.lnf_b), ptr(self.freqs), ptr(ws["x"]), ptr(ws["xn"]),
+                               ptr(ws["y"]), ptr(ws["h"]), ptr(ws["part"]), ptr(ws["attn_work"]), ptr(ws["yz"]),
+                               ptr(ws["ym"]), ptr(ws["xc"]), ptr(ws["dbg"]), st, sp)
+
+    def _c_decode(self, ws, B, st, sp, stream):
+        call("zk_hybrid_decode_step", C.byref(self._step_desc(ws, B, st, sp)), stream)
+
+    def _c_prefill(self, ws, B, st, sp, cond, Lc, P, stream):
+        call("zk_hybrid_prefill", C.byref(self._step_desc(ws, B, st, sp)), ptr(cond), Lc, P, ptr(ws["q"]), stream)
 
     # ------------------------------------------------------------------ layer loop
     def _layers(self, ws, M: int, R: int, S: int, prefill: bool, stream, skip):
