@@ -8,9 +8,10 @@ pyloudnorm 0.1.1's published algorithm (ITU-R BS.1770-4): `Meter(rate, block_siz
 with the "K-weighting" filter = high shelf (G 4 dB, Q 1/sqrt(2), fc 1500 Hz) then high pass
 (G 0, Q 0.5, fc 38 Hz), RBJ-cookbook biquads applied with scipy.signal.lfilter in float64;
 400 ms (or 100 ms for short audio) gating blocks with 75 % overlap; absolute gate
--70 LUFS, relative gate -10 LU; channel weight 1.0 (mono). Parity of this restatement with
-pyloudnorm itself is UNPINNED (the library is absent and no fixture from it exists); it is
-anchored on the reference's call site (autoencoder.py:175-181: block size rule, target,
+-70 LUFS, relative gate -10 LU; channel weight 1.0 (mono). pyloudnorm itself is absent and no
+fixture from it exists, so parity is pinned to the standard it implements instead: EBU Tech
+3341's known-answer cases 1-5 (tests/loudness_kat.py, +-0.1 LU, tests/test_loudness_kat_cpu.py),
+and anchored on the reference's call site (autoencoder.py:175-181: block size rule, target,
 gain = 10**((target - loudness)/20), exception -> unchanged audio).
 """
 from __future__ import annotations

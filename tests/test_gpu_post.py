@@ -75,3 +75,18 @@ def test_save_codes_writes_float_wav(tmp_path):
     w = ae.codes_to_wavs(codes[0])[0]
     data = np.frombuffer(raw[raw.index(b"data") + 8:], dtype="<f4")
     assert np.array_equal(data, w.numpy().reshape(-1))
+
+
+def test_loudness_gpu_ebu3341_known_answers():
+    """The batched GPU meter (post.hip) on EBU Tech 3341 cases 1-5 (tests/loudness_kat.py): the
+    integrated loudness it implies (target - 20 log10 gain) is the standard's answer within
+    +-0.1 LU -- pins the meter to BS.1770-4 / EBU R 128 (pyloudnorm itself is absent)."""
+    from .loudness_kat import EBU3341, ebu_expected_mono, ebu_signal
+    ae, _ = _ae()
+    sr = ae.sampling_rate
+    cases = sorted(EBU3341)
+    wavs = [torch.from_numpy(ebu_signal(c, sr)).float().unsqueeze(0) for c in cases]
+    gains = ae.loudness_gains(wavs, -23.0)
+    for c, g in zip(cases, gains):
+        loud = -23.0 - 20.0 * math.log10(g)
+        assert abs(loud - ebu_expected_mono(c)) <= 0.1, (c, loud, ebu_expected_mono(c))
