@@ -286,9 +286,9 @@ def dac():
     from zonos_amd import synthetic
     from zonos_amd.autoencoder import DacSpec, HipDacDecoder
     W = synthetic.dac_weights(dev)
-    for prec in ("fp32", "fp16x3", "fp16"):
+    for prec in os.environ.get("ZK_MB_DAC_PREC", "fp16").split(","):
         d = HipDacDecoder(DacSpec(), W, dev, precision=prec)
-        for B, T in ((8, 256),):
+        for B, T in ((8, 256), (16, 2580)):
             codes = torch.randint(0, 1024, (B, 9, T), device=dev)
             us = timeit(lambda: d.decode_padded(codes), reps=3, warm=1)
             fl = 1.6083e9 * B * T

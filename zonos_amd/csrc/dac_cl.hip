@@ -78,9 +78,16 @@ ZK_DEV void wait_vm(int n) {
 #undef ZK_W1
 }
 
-constexpr int CL_DA = 3;                 // weight slices in flight ahead of the step being computed
+#ifndef ZK_CL_DA
+#define ZK_CL_DA 3
+#endif
+constexpr int CL_DA = ZK_CL_DA;          // weight slices in flight ahead of the step being computed
 constexpr int CL_NW = CL_DA + 2;         // weight ring slots
-constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
+#ifndef ZK_CL_NLD
+#define ZK_CL_NLD 2
+#endif
+constexpr int CL_NLD = ZK_CL_NLD;        // loader waves (LDS-DMA issue is the per-step limit with one)
+constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 
 // Loader-wave implicit GEMM. Wave 4 only moves bytes (LDS-DMA) and counts its own vmcnt;
 // waves 0-3 only read LDS + MFMA, so the vmcnt(0) that hipcc places before their ds_reads
@@ -90,7 +97,7 @@ constexpr int CL_THREADS = 320;          // 4 compute waves + 1 loader wave
 // DA: weight slices the loader keeps in flight (ring of DA + 2 slots); OCC: workgroups per CU the
 // registers are sized for
 template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2>
-__global__ __launch_bounds__(CL_THREADS, OCC) void k_conv_cl(
+__global__ __launch_bounds__(CL_THREADS, (OCC * CL_THREADS + 255) / 256) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
     int out_off0, int Tout, const float* resid, float* xout, const float* __restrict__ alpha,
@@ -122,8 +129,9 @@ __global__ __launch_bounds__(CL_THREADS, OCC) void k_conv_cl(
     char* const xring = smem + (DA + 2) * WS;
     const int nchunk = Cin / CI, nstep = nchunk * ks;
 
-    if (wv == 4) {
-        // ---------------- loader wave
+    if (wv >= 4) {
+        // ---------------- loader waves: loader lw moves the pieces p with p % CL_NLD == lw
+        const int lw = wv - 4;
         const int len_in = lens ? min(lens[b] * in_scale, Tin) : Tin;
         const uint16_t* wp = w + (size_t)phase * wphase;
         const size_t wtap = (size_t)Cout * Cin;
@@ -139,7 +147,7 @@ __global__ __launch_bounds__(CL_THREADS, OCC) void k_conv_cl(
             if (sx >= 0 && sx < nstep && sx % ks == 0) {
                 const int c = sx / ks;
                 char* dst = xring + (c % nx_slots) * XS;
-                for (int p = 0; p < nxp; ++p) {
+                for (int p = lw; p < nxp; p += CL_NLD) {
                     const int row = p * 16 + prow;
                     const int u = u0 + row;
                     const int g = pslot ^ I::swz(row);
@@ -148,7 +156,7 @@ __global__ __launch_bounds__(CL_THREADS, OCC) void k_conv_cl(
                                           : (const void*)g_zero_page;
                     __builtin_amdgcn_global_load_lds(src, (void*)(dst + p * 1024), 16, 0, 0);
                 }
-                nl += nxp;
+                nl += (nxp - lw + CL_NLD - 1) / CL_NLD;
             }
             const int sw = j + DA;
             if (sw >= 0 && sw < nstep) {
@@ -156,13 +164,15 @@ __global__ __launch_bounds__(CL_THREADS, OCC) void k_conv_cl(
                 char* dst = wring + (sw % (DA + 2)) * WS;
                 const uint16_t* src0 = wp + t * wtap + (size_t)co0 * Cin + c * CI;
 #pragma unroll
-                for (int p = 0; p < NWP; ++p) {
+                for (int pp = 0; pp < (NWP + CL_NLD - 1) / CL_NLD; ++pp) {
+                    const int p = pp * CL_NLD + lw;
+                    if (p >= NWP) break;
                     const int row = p * 16 + prow;
                     const int g = pslot ^ I::swz(row);
                     __builtin_amdgcn_global_load_lds((const void*)(src0 + (size_t)row * Cin + g * 8),
                                                      (void*)(dst + p * 1024), 16, 0, 0);
                 }
-                nl += NWP;
+                nl += (NWP - lw + CL_NLD - 1) / CL_NLD;
             }
 #pragma unroll
             for (int k = 0; k < DA; ++k) hist[k] = hist[k + 1];
