@@ -14,6 +14,7 @@ from zonos_amd import _lib, autoencoder, synthetic  # noqa: E402
 from zonos_amd.autoencoder import DacSpec, HipDacDecoder  # noqa: E402
 
 _lib.load()
+HipDacDecoder.c_dac = False      # per-launch timing needs the Python-issued sequence
 dev = torch.device("cuda")
 S = _lib.stream_ptr()
 e0, e1 = _lib.P(), _lib.P()
