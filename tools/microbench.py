@@ -33,8 +33,12 @@ def timeit(fn, reps=50, warm=5):
 
 def gemm():
     M = int(os.environ.get("ZK_MB_M", "128"))
-    for name, N, K, mode in (("qkv", 3072, 2048, 0), ("o", 2048, 2048, 0), ("fc1", 16384, 2048, 1),
-                             ("fc2", 2048, 8192, 0), ("heads", 9234, 2048, 0)):
+    shapes = [("qkv", 3072, 2048, 0), ("o", 2048, 2048, 0), ("fc1", 16384, 2048, 1),
+              ("fc2", 2048, 8192, 0), ("heads", 9234, 2048, 0)]
+    # extra shapes "name:N:K:mode,..." (e.g. fc1 as a split-K slab GEMM: "fc1s:16384:2048:0")
+    shapes += [(t[0], int(t[1]), int(t[2]), int(t[3])) for t in
+               (x.split(":") for x in os.environ.get("ZK_MB_GEMM_EXTRA", "").split(",") if x)]
+    for name, N, K, mode in shapes:
         # distinct weight buffers per rep set so L2/MALL does not serve them: rotate 8 copies (>256 MB total)
         ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
         Npad = (N + 63) // 64 * 64        # packed layout reads whole 64-row tiles
