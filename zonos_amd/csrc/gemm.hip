@@ -231,7 +231,6 @@ constexpr int WS_DA = ZK_WS_DA;  // activation chunks in flight (loader); WS_NB 
 #define ZK_WS_NLD 4
 #endif
 constexpr int WS_NLD = ZK_WS_NLD;            // loader waves (each moves 1/WS_NLD of every chunk)
-constexpr int WS_THREADS = 256 + 64 * WS_NLD;
 #ifndef ZK_WS_PF
 #define ZK_WS_PF 4
 #endif
@@ -268,8 +267,8 @@ ZK_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory")
 
 // MT = 16-row M tiles actually present (1, 2, 4, 8): small batches stage and multiply only
 // the rows they have (B = 1 decode: 2 rows -> one 16-row tile instead of 8).
-template <int MODE, int NCH, int PF, int MT>
-__global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
+template <int MODE, int NCH, int PF, int MT, int NCW = 4>
+__global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
                                                            bf16_t* __restrict__ Cout, const int32_t* skip) {
@@ -289,19 +288,20 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         bx = I - bz * gridDim.x;
     }
 #endif
-    const int n0 = bx * BN, split = bz;
+    constexpr int BNW = 16 * NCW;                 // columns per workgroup (16 per compute wave)
+    const int n0 = bx * BNW, split = bz;
     const int kbeg = split * kslice;
     const int nchunks = kslice / BK;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int ln = lane & 15, lg = lane >> 4;
 
-    if (w >= 4) {
+    if (w >= NCW) {
         // ---------------- loader wave(s): 2*MT x 1 KB LDS-DMA pieces per chunk (16*MT rows x 64 k),
         // loader l moving pieces l, l + WS_NLD, ...
         // piece i covers tile rows 8i..8i+7; lane L lands at byte 16L of the piece:
         // row = 8i + (L>>3), slot = L&7  ->  source 16-B chunk = slot ^ (row&7)
         constexpr int NP = (2 * MT + WS_NLD - 1) / WS_NLD;      // pieces per loader per chunk
-        const int ld = w - 4;
+        const int ld = w - NCW;
         const int rl = lane >> 3, sl = lane & 7;
         auto issue = [&](int ch) {
             char* dst = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
@@ -341,7 +341,9 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
     // ---------------- compute waves
     const int wn = n0 + w * 16 + ln;
     const bool wvalid = wn < N;
-    const bf16_t* wrow = w_base(W, n0 + w * 16, wvalid ? wn : 0, K, kbeg, lane);
+    // a 16-row tile wholly past N streams tile 0 (never stored): the packed image ends at ceil64(N)
+    const int trow = n0 + w * 16 < N ? n0 + w * 16 : 0;
+    const bf16_t* wrow = w_base(W, trow, wvalid ? wn : 0, K, kbeg, lane);
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -358,7 +360,9 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
     }
     // activation fragments of the next chunk are read from LDS (register double buffer) while
     // the current chunk is multiplied: the LDS latency after each barrier is off the MFMA path
-    uint4 af[2][2][MT];
+    // (NCW > 4: 3 waves per SIMD leave 168 VGPRs -- one fragment set, read after the MFMAs)
+    constexpr int NB = NCW > 4 ? 1 : 2;
+    uint4 af[NB][2][MT];
     auto read_frags = [&](int ch, int buf) {
         const char* base = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
 #pragma unroll
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
             wr0[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH);
             wr1[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH + WHALF);
         }
-        if (ch + 1 < NCH) {
+        if (NB == 2 && ch + 1 < NCH) {
             __builtin_amdgcn_s_barrier();                           // chunk ch+1 (and ch+2) in LDS
             asm volatile("" ::: "memory");
             read_frags(ch + 1, (ch + 1) & 1);
@@ -387,7 +391,14 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
             const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(af[ch & 1][ks][mt]), b, acc[mt], 0, 0, 0);
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(af[NB == 2 ? (ch & 1) : 0][ks][mt]), b,
+                                                                  acc[mt], 0, 0, 0);
+        }
+        if (NB == 1 && ch + 1 < NCH) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();                           // chunk ch+1 (and ch+2) in LDS
+            asm volatile("" ::: "memory");
+            read_frags(ch + 1, 0);
         }
     }
     if (ZK_WS_EPI && (MODE == 1 || N % 4 == 0)) {
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
         // whole rows: slabs 4 rows x 256 B (full 128-B lines) per instruction instead of 4 x 64-B
         // pieces, SwiGLU 16 rows x 64 B instead of 16-B pieces. (The loader waves have exited; a
         // workgroup barrier no longer counts them.)
-        constexpr int TS = 68;                                   // fp32 tile row stride (64 + pad)
+        constexpr int TS = BNW + 4;                              // fp32 tile row stride (+ pad)
         float* tile = reinterpret_cast<float*>(smem);
         __syncthreads();                                         // every wave's last LDS fragment read
         if (MODE == 0) {
@@ -404,25 +415,22 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
 #pragma unroll
                 for (int i = 0; i < 4; ++i) tile[(mt * 16 + lg * 4 + i) * TS + w * 16 + ln] = acc[mt][i];
         } else {
+            // the bf16-rounded y / gate columns as they are (8 + 8 interleaved per 16-column group);
+            // SwiGLU runs in the store pass below, on every lane (here it would run on half the lanes
+            // behind a branch per value: fc1 23.4 -> 18.x us)
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float mine = round_bf(acc[mt][i]);
-                    const float other = __shfl_xor(mine, 8, 64);
-                    if (ln < 8) {
-                        const float sl = round_bf(other / (1.0f + expf(-other)));
-                        tile[(mt * 16 + lg * 4 + i) * TS + w * 8 + ln] = mine * sl;   // 32 output columns
-                    }
-                }
+                for (int i = 0; i < 4; ++i) tile[(mt * 16 + lg * 4 + i) * TS + w * 16 + ln] = round_bf(acc[mt][i]);
         }
         __syncthreads();
         if (MODE == 0) {
             float* C = Cpart + (size_t)split * M * N;
-            const int c4 = (lane & 15) * 4;
+            constexpr int LPR = 4 * NCW;                         // lanes per row (4 floats each)
+            const int c4 = (lane % LPR) * 4;
 #pragma unroll
-            for (int q = w; q < MT * 4; q += 4) {               // 4 rows x 256 B per instruction
-                const int m = q * 4 + (lane >> 4);
+            for (int q = w; q < MT * NCW; q += NCW) {           // 64 / LPR whole rows per instruction
+                const int m = q * (64 / LPR) + lane / LPR;
                 if (m < M && n0 + c4 < N) {
                     const f32x4 v = *reinterpret_cast<const f32x4*>(tile + m * TS + c4);
                     float* dst = C + (size_t)m * N + n0 + c4;
@@ -438,13 +446,20 @@ __global__ __launch_bounds__(WS_THREADS, ZK_WS_OCC) void k_gemm_ws(const bf16_t*
             }
         } else {
             const int F = N / 2;
-            const int f0 = n0 / 2, c8 = (lane & 3) * 8;
+            const int f0 = n0 / 2, gi = lane % NCW;             // 16-column group gi -> outputs f0 + 8 gi ..
 #pragma unroll
-            for (int q = w; q < MT; q += 4) {                    // 16 rows x 64 B per instruction
-                const int m = q * 16 + (lane >> 2);
-                if (m < M && f0 + c8 < F) {
-                    const float* src = tile + m * TS + c8;
-                    *reinterpret_cast<uint4*>(Cout + (size_t)m * F + f0 + c8) = pack8(src);
+            for (int q = w; q < MT * NCW / 4; q += NCW) {        // 64 / NCW rows x 16*NCW B per instruction
+                const int m = q * (64 / NCW) + lane / NCW;
+                if (m < M && f0 + gi * 8 < F) {
+                    const float* yv = tile + m * TS + gi * 16;
+                    float o[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float g = yv[8 + j];
+                        const float sl = round_bf(g / (1.0f + expf(-g)));     // F.silu in bf16
+                        o[j] = yv[j] * sl;
+                    }
+                    *reinterpret_cast<uint4*>(Cout + (size_t)m * F + f0 + gi * 8) = pack8(o);
                 }
             }
         }
@@ -924,15 +939,20 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
         }
     }
     if (M <= BM && nchunks <= 32) {
-        dim3 g((N + BN - 1) / BN, 1, nsplit);
+#ifndef ZK_WS_NCW
+#define ZK_WS_NCW 4
+#endif
+        constexpr int NCW = ZK_WS_NCW;            // compute waves = 16-column tiles per workgroup
+        dim3 g((N + 16 * NCW - 1) / (16 * NCW), 1, nsplit);
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
         const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2;
 #define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
     do {                                                                                                          \
         if (lds > 65536)                                                                                          \
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, WS_PF, MT_>),               \
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, WS_PF, MT_, NCW>),          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
-        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, WS_PF, MT_>), g, dim3(WS_THREADS), lds, (hipStream_t)stream,   \
+        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, WS_PF, MT_, NCW>), g, dim3(64 * (NCW + WS_NLD)), lds,          \
+                           (hipStream_t)stream,                                                                   \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
                            skip_flag);                                                                             \
         handled = true;                                                                                           \
