@@ -55,14 +55,18 @@ __global__ void k_dma(const uint4* __restrict__ W, uint32_t* out) {
 // 4*blk + w, two register sets in flight). ROT: each workgroup starts at a different key block
 // (address stagger); ADJ: K and V slices adjacent in one array (16 KB contiguous per slice).
 struct Frag { uint4 k[8]; uint4 v[8]; };
-template <bool ADJ>
+template <bool ADJ, bool NTL = false>
 __device__ __forceinline__ void ld(Frag& f, const char* kb, const char* vb, int slice, int lane) {
     const char* k0 = ADJ ? kb + (size_t)slice * 16384 + lane * 16 : kb + (size_t)slice * 8192 + lane * 16;
     const char* v0 = ADJ ? k0 + 8192 : vb + (size_t)slice * 8192 + lane * 16;
+    auto g = [](const char* a) -> uint4 {
+        if constexpr (NTL) return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a)));
+        else return *reinterpret_cast<const uint4*>(a);
+    };
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f.k[i] = *reinterpret_cast<const uint4*>(k0 + i * 1024);
+    for (int i = 0; i < 8; ++i) f.k[i] = g(k0 + i * 1024);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f.v[i] = *reinterpret_cast<const uint4*>(v0 + i * 1024);
+    for (int i = 0; i < 8; ++i) f.v[i] = g(v0 + i * 1024);
 }
 __device__ __forceinline__ uint32_t eat(const Frag& f) {
     uint32_t a = 0;
@@ -70,7 +74,33 @@ __device__ __forceinline__ uint32_t eat(const Frag& f) {
     for (int i = 0; i < 8; ++i) a ^= f.k[i].x ^ f.k[i].w ^ f.v[i].y ^ f.v[i].z;
     return a;
 }
-template <bool ROT, bool ADJ, int SPLIT = 1>
+// same access shape moved by LDS-DMA (no consumer): every wave streams its slices 1 KB at a time into its own
+// RING-slot LDS ring, RING-1 KB in flight; AUX 2 = nt, 0 = default policy
+template <int RING, int AUX>
+__global__ __launch_bounds__(256, 2) void k_att_dma(const char* K, const char* V, int ctx, size_t region, uint32_t* out) {
+    extern __shared__ char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int unit = blockIdx.x;
+    const int nblk = (ctx + 127) / 128;
+    const char* kb = K + unit * region;
+    const char* vb = V + unit * region;
+    char* ring = smem + w * RING * 1024;
+    int n = 0;
+    for (int b = 0; b < nblk; ++b) {
+        const int slice = 4 * b + w;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const char* src = (i < 8 ? kb + (size_t)slice * 8192 + i * 1024 : vb + (size_t)slice * 8192 + (i - 8) * 1024) + lane * 16;
+            __builtin_amdgcn_global_load_lds((const void*)src, (void*)(ring + (n % RING) * 1024), 16, 0, AUX);
+            ++n;
+            if (n >= RING - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RING - 2) : "memory");
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (reinterpret_cast<uint32_t*>(ring)[lane] == 0x12345678u) out[0] = 1;
+}
+
+template <bool ROT, bool ADJ, int SPLIT = 1, bool NTL = false>
 __global__ __launch_bounds__(256, 2) void k_att(const char* K, const char* V, int ctx, size_t region, uint32_t* out) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int unit = blockIdx.x / SPLIT, part = blockIdx.x % SPLIT;
@@ -83,11 +113,11 @@ __global__ __launch_bounds__(256, 2) void k_att(const char* K, const char* V, in
     auto sl = [&](int b) { b = b < nblk ? b : nblk - 1; b += rot; b -= b >= nblk ? nblk : 0; return 4 * b + w; };
     Frag fa, fb;
     uint32_t acc = 0;
-    ld<ADJ>(fa, kb, vb, sl(0), lane);
+    ld<ADJ, NTL>(fa, kb, vb, sl(0), lane);
     for (int it = 0; it < nblk; it += 2) {
-        ld<ADJ>(fb, kb, vb, sl(it + 1), lane);
+        ld<ADJ, NTL>(fb, kb, vb, sl(it + 1), lane);
         acc ^= eat(fa);
-        ld<ADJ>(fa, kb, vb, sl(it + 2), lane);
+        ld<ADJ, NTL>(fa, kb, vb, sl(it + 2), lane);
         if (it + 1 < nblk) acc ^= eat(fb);
     }
     if (acc == 0x12345678u) out[0] = acc;
@@ -100,11 +130,12 @@ int att_probe(char* big, size_t total, uint32_t* out, hipEvent_t e0, hipEvent_t 
     for (int ctx : {512, 1705, 2999}) {
         const double bytes = 512.0 * ctx * 512;
         int grid_mult = 1;
+        size_t lds = 0;
         auto go = [&](const char* name, auto kern) -> int {
             const int grid = 512 * (int)grid_mult;
-            for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, K, V, ctx, region, out);
+            for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, K, V, ctx, region, out);
             CK(hipEventRecord(e0, 0));
-            for (int i = 0; i < 50; ++i) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, K, V, ctx, region, out);
+            for (int i = 0; i < 50; ++i) hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, K, V, ctx, region, out);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float ms;
@@ -114,11 +145,19 @@ int att_probe(char* big, size_t total, uint32_t* out, hipEvent_t e0, hipEvent_t 
             return 0;
         };
         go("base", k_att<false, false>);
-        go("adj+rot", k_att<true, true>);
-        grid_mult = 2; go("split2", k_att<false, false, 2>);
-        grid_mult = 4; go("split4", k_att<false, false, 4>);
-        grid_mult = 8; go("split8", k_att<false, false, 8>);
-        grid_mult = 1;
+        go("base-nt", k_att<false, false, 1, true>);
+        if (getenv("ATT_ALL")) {
+            go("adj+rot", k_att<true, true>);
+            grid_mult = 2; go("split2", k_att<false, false, 2>);
+            grid_mult = 4; go("split4", k_att<false, false, 4>);
+            grid_mult = 8; go("split8", k_att<false, false, 8>);
+            grid_mult = 1;
+        }
+        lds = 4 * 8 * 1024; go("dma8-nt", k_att_dma<8, 2>);
+        lds = 4 * 16 * 1024; go("dma16-nt", k_att_dma<16, 2>);
+        go("dma16", k_att_dma<16, 0>);
+        lds = 4 * 20 * 1024; go("dma20-nt", k_att_dma<20, 2>);
+        lds = 0;
     }
     (void)total;
     return 0;
