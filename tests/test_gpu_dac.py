@@ -96,3 +96,28 @@ def test_c_dac_decode_equals_python_sequence(name, monkeypatch):
         monkeypatch.setattr(HipDacDecoder, "c_dac", flag)
         outs.append(dec.decode_padded(codes2, lens).cpu())
     assert outs[0].shape == outs[1].shape and torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("C", [16, 96])
+def test_tail_conv_matches_fp32_conv(C):
+    """zk_dac_tail_cl (final Snake output -> Conv1d(C, 1, 7, pad 3) -> tanh, modeling_dac.py:437-439)
+    against torch's fp32 conv1d on the same channels-last input, with ragged row lengths and
+    positions that straddle the 128-position workgroup tiles; zero beyond each row's length."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    g = torch.Generator().manual_seed(C)
+    B, T = 3, 1000
+    lens = torch.tensor([1000, 517, 129], dtype=torch.int32)
+    s = torch.randn(B, T, C, generator=g)
+    for b in range(B):
+        s[b, int(lens[b]):] = 0.0                      # the producer conv zeroes the tail of a row
+    w = torch.randn(1, C, 7, generator=g) * 0.1
+    bias = torch.randn(1, generator=g) * 0.1
+    ref = torch.tanh(torch.nn.functional.conv1d(s.transpose(1, 2).double(), w.double(), bias.double(), padding=3))[:, 0]
+    for b in range(B):
+        ref[b, int(lens[b]):] = 0.0
+    out = torch.full((B, T), 7.0, device="cuda")
+    sd, wd, bd, ld = s.cuda(), w[0].contiguous().cuda(), bias.cuda(), lens.cuda()
+    call("zk_dac_tail_cl", ptr(sd), B, C, T, ptr(wd), ptr(bd), ptr(out), ptr(ld), 1, stream_ptr())
+    torch.cuda.synchronize()
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err < 1e-5, err

@@ -81,6 +81,12 @@ ZK_DEV void wait_vm(int n) {
 #ifndef ZK_CL_DA
 #define ZK_CL_DA 3
 #endif
+#ifndef ZK_CL_DIAG_NOW             // diagnostic builds only: weight slices loaded once (stale data)
+#define ZK_CL_DIAG_NOW 0
+#endif
+#ifndef ZK_CL_DIAG_NOMFMA          // diagnostic builds only: no MFMAs (wrong results)
+#define ZK_CL_DIAG_NOMFMA 0
+#endif
 constexpr int CL_DA = ZK_CL_DA;          // weight slices in flight ahead of the step being computed
 constexpr int CL_NW = CL_DA + 2;         // weight ring slots
 #ifndef ZK_CL_NLD
@@ -97,7 +103,10 @@ constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 // DA: weight slices the loader keeps in flight (ring of DA + 2 slots); OCC: workgroups per CU the
 // registers are sized for
 template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2>
-__global__ __launch_bounds__(CL_THREADS, (OCC * CL_THREADS + 255) / 256) void k_conv_cl(
+#ifndef ZK_CL_LBW
+#define ZK_CL_LBW(OCC_) ((OCC_ * CL_THREADS + 255) / 256)
+#endif
+__global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
     int out_off0, int Tout, const float* resid, float* xout, const float* __restrict__ alpha,
@@ -131,7 +140,10 @@ __global__ __launch_bounds__(CL_THREADS, (OCC * CL_THREADS + 255) / 256) void k_
 
     if (wv >= 4) {
         // ---------------- loader waves: loader lw moves the pieces p with p % CL_NLD == lw
-        const int lw = wv - 4;
+        // wave-uniform (readfirstlane): the piece counts and the vmcnt switch below stay scalar;
+        // derived from threadIdx they would be per-lane values and the 64-way wait_vm switch a
+        // chain of exec-masked branches (the loader then paced every step: convs +20 %)
+        const int lw = __builtin_amdgcn_readfirstlane(wv - 4);
         const int len_in = lens ? min(lens[b] * in_scale, Tin) : Tin;
         const uint16_t* wp = w + (size_t)phase * wphase;
         const size_t wtap = (size_t)Cout * Cin;
@@ -159,7 +171,7 @@ __global__ __launch_bounds__(CL_THREADS, (OCC * CL_THREADS + 255) / 256) void k_
                 nl += (nxp - lw + CL_NLD - 1) / CL_NLD;
             }
             const int sw = j + DA;
-            if (sw >= 0 && sw < nstep) {
+            if (!ZK_CL_DIAG_NOW && sw >= 0 && sw < nstep) {
                 const int c = sw / ks, t = sw - c * ks;
                 char* dst = wring + (sw % (DA + 2)) * WS;
                 const uint16_t* src0 = wp + t * wtap + (size_t)co0 * Cin + c * CI;
@@ -167,6 +179,18 @@ __global__ __launch_bounds__(CL_THREADS, (OCC * CL_THREADS + 255) / 256) void k_
                 for (int pp = 0; pp < (NWP + CL_NLD - 1) / CL_NLD; ++pp) {
                     const int p = pp * CL_NLD + lw;
                     if (p >= NWP) break;
+                    const int row = p * 16 + prow;
+                    const int g = pslot ^ I::swz(row);
+                    __builtin_amdgcn_global_load_lds((const void*)(src0 + (size_t)row * Cin + g * 8),
+                                                     (void*)(dst + p * 1024), 16, 0, 0);
+                }
+                nl += (NWP - lw + CL_NLD - 1) / CL_NLD;
+            }
+            if (ZK_CL_DIAG_NOW && sw >= 0 && sw < nstep && sw < DA + 2) {      // diag: fill each weight slot once
+                const int c = sw / ks, t = sw - c * ks;
+                char* dst = wring + (sw % (DA + 2)) * WS;
+                const uint16_t* src0 = wp + t * wtap + (size_t)co0 * Cin + c * CI;
+                for (int p = lw; p < NWP; p += CL_NLD) {
                     const int row = p * 16 + prow;
                     const int g = pslot ^ I::swz(row);
                     __builtin_amdgcn_global_load_lds((const void*)(src0 + (size_t)row * Cin + g * 8),
@@ -227,11 +251,18 @@ __global__ __launch_bounds__(CL_THREADS, (OCC * CL_THREADS + 255) / 256) void k_
 #pragma unroll
         for (int n = 0; n < NQ; ++n)
             bq[n] = *reinterpret_cast<const uint4*>(xb + I::off(wn * 16 * NQ + n * 16 + ln + t * dil, lg));
+        if (ZK_CL_DIAG_NOMFMA) {          // diag: keep the operand reads, drop the MFMAs
 #pragma unroll
-        for (int m = 0; m < FM; ++m)
+            for (int m = 0; m < FM; ++m)
 #pragma unroll
-            for (int n = 0; n < NQ; ++n)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a[m]), as_h8(bq[n]), acc[m][n], 0, 0, 0);
+                for (int n = 0; n < NQ; ++n) acc[m][n][0] += __uint_as_float(a[m].x ^ bq[n].y);
+        } else {
+#pragma unroll
+            for (int m = 0; m < FM; ++m)
+#pragma unroll
+                for (int n = 0; n < NQ; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a[m]), as_h8(bq[n]), acc[m][n], 0, 0, 0);
+        }
     }
 
     // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 16NQ wn + 16n + ln]
@@ -309,21 +340,37 @@ __global__ __launch_bounds__(256) void k_rvq_cl(const int64_t* __restrict__ code
 // out[b][t] = tanh(b + sum_{c,k} w[c][k] s[t+k-3][c]) from the channels-last fp32 Snake output
 // of the last residual unit (modeling_dac.py:437-439; one output channel, so VALU: an MFMA
 // tile would be 1/16 used). fp32 here keeps the waveform within the fp32 reference's 1e-4.
-constexpr int TAIL_T = 256;
-__global__ __launch_bounds__(256) void k_tail_cl(const float* __restrict__ s, int C, int T,
-                                                 const float* __restrict__ w, const float* __restrict__ bias,
-                                                 float* __restrict__ out, const int32_t* __restrict__ lens, int scale) {
-    extern __shared__ float wl[];            // [C][7]
-    for (int i = threadIdx.x; i < C * 7; i += 256) wl[i] = w[i];
-    __syncthreads();
-    const int b = blockIdx.y, t = blockIdx.x * TAIL_T + threadIdx.x;
-    if (t >= T) return;
+// The TAIL_T + 6 input rows of a workgroup are one contiguous [rows][C] block: staged into LDS
+// by whole float4 loads (row stride C + 4 floats: the 16 lanes of a ds_read_b128 hit distinct
+// banks), then each thread sums its position's 7 x C products in the order k, c.
+constexpr int TAIL_T = 128;
+__global__ __launch_bounds__(TAIL_T) void k_tail_cl(const float* __restrict__ s, int C, int T,
+                                                    const float* __restrict__ w, const float* __restrict__ bias,
+                                                    float* __restrict__ out, const int32_t* __restrict__ lens,
+                                                    int scale) {
+    extern __shared__ __attribute__((aligned(16))) float tl[];     // [C][7] weights, then [TAIL_T + 6][C + 4] rows
+    const int CS = C + 4, C4 = C / 4;
+    float* wl = tl;
+    float* rows = tl + ((C * 7 + 3) & ~3);
+    const int b = blockIdx.y, t0 = blockIdx.x * TAIL_T;
     const int len = lens ? min(lens[b] * scale, T) : T;
+    for (int i = threadIdx.x; i < C * 7; i += TAIL_T) wl[i] = w[i];
+    const float4* src = reinterpret_cast<const float4*>(s + (size_t)b * T * C);
+    const int nrow = TAIL_T + 6;
+    for (int i = threadIdx.x; i < nrow * C4; i += TAIL_T) {
+        const int r = i / C4, c4 = i - r * C4;
+        const int u = t0 - 3 + r;
+        const float4 v = (u >= 0 && u < len) ? src[(size_t)u * C4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(rows + r * CS + 4 * c4) = v;
+    }
+    __syncthreads();
+    const int t = t0 + threadIdx.x;
+    if (t >= T) return;
     float acc = 0.f;
     for (int k = 0; k < 7; ++k) {
         const int u = t + k - 3;
         if (u < 0 || u >= len) continue;
-        const float* row = s + ((size_t)b * T + u) * C;
+        const float* row = rows + (threadIdx.x + k) * CS;
         for (int c = 0; c < C; c += 4) {
             const float4 v = *reinterpret_cast<const float4*>(row + c);
             acc = fmaf(wl[(c + 0) * 7 + k], v.x, acc);
@@ -564,9 +611,11 @@ extern "C" int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* 
                               const int32_t* lens, int scale, void* stream) {
     ZK_REQUIRE(C > 0 && C % 4 == 0 && T >= 0, "zk_dac_tail_cl: bad shape C=%d", C);
     if (B == 0 || T == 0) return 0;
-    const size_t lds = (size_t)C * 7 * sizeof(float);
-    ZK_REQUIRE(lds <= 64 * 1024, "zk_dac_tail_cl: C=%d too large", C);
-    hipLaunchKernelGGL(k_tail_cl, dim3((T + TAIL_T - 1) / TAIL_T, B), dim3(256), lds, (hipStream_t)stream, s, C, T, w,
+    const size_t lds = ((size_t)((C * 7 + 3) & ~3) + (size_t)(TAIL_T + 6) * (C + 4)) * sizeof(float);
+    ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_tail_cl: C=%d too large", C);
+    if (lds > 65536)
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tail_cl), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_tail_cl, dim3((T + TAIL_T - 1) / TAIL_T, B), dim3(TAIL_T), lds, (hipStream_t)stream, s, C, T, w,
                        bias, out, lens, scale);
     ZK_CHECK_LAUNCH("zk_dac_tail_cl");
     return 0;

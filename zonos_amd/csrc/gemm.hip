@@ -301,7 +301,7 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
         // piece i covers tile rows 8i..8i+7; lane L lands at byte 16L of the piece:
         // row = 8i + (L>>3), slot = L&7  ->  source 16-B chunk = slot ^ (row&7)
         constexpr int NP = (2 * MT + WS_NLD - 1) / WS_NLD;      // pieces per loader per chunk
-        const int ld = w - NCW;
+        const int ld = __builtin_amdgcn_readfirstlane(w - NCW);   // wave-uniform: scalar piece loop
         const int rl = lane >> 3, sl = lane & 7;
         auto issue = [&](int ch) {
             char* dst = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
