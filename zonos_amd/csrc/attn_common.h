@@ -256,7 +256,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
     const int nkb = (ctx + AT_KB - 1) / AT_KB;
     const int kb0 = (int)((long)split * nkb / nsplit), kb1 = (int)((long)(split + 1) * nkb / nsplit);
     const int G = H / Hkv;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
     bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;

@@ -29,7 +29,7 @@ namespace {
 // partial-sum slot per wave for the mean and one for the variance: one barrier per reduction).
 template <int NT, int n8>
 ZK_DEV void ln_row_pre(const float* x, const uint4* wv, const uint4* bv, float eps, int D, bf16_t* y, float* red) {
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < n8; ++j)
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(512) void k_resid_ln_d2k512(const float* part, int 
 #pragma unroll
         for (int e = 0; e < 4; ++e) xv[e] = round_bf(xv[e]);
     }
-    const int wv = t >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     float sum = xv[0] + xv[1] + xv[2] + xv[3];
     sum = wave_sum(sum);
     if ((t & 63) == 0) red[wv] = sum;
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(64) void k_attn_combine(const float* work, int H, i
 __global__ __launch_bounds__(256) void k_attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vt, int R,
                                                       int S, int H, int Hkv, int Smax, float scale, bf16_t* out) {
     constexpr int HD = 128;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int h = blockIdx.y, r = blockIdx.z;
     const int q0 = blockIdx.x * 64 + w * 16;               // this wave's first query

@@ -55,7 +55,7 @@ ZK_DEV float wave_max(float v) {
 template <int NT>
 ZK_DEV float block_sum(float v, float* red) {
     v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[w] = v;
     __syncthreads();
@@ -67,7 +67,7 @@ ZK_DEV float block_sum(float v, float* red) {
 template <int NT>
 ZK_DEV float block_max(float v, float* red) {
     v = wave_max(v);
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[w] = v;
     __syncthreads();

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
     constexpr int QTT = 32 * NQ;
     const int q0 = qtile * QTT;
 
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int win = QTT + (ks - 1) * dil;
     const int nxp = (win + 15) >> 4;             // window pieces (16 rows each)
     const int XS = nxp * 1024;
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(256) void k_rvq_encode(const float* __restrict__ z,
     __shared__ int besti[4];
     __shared__ float qv[RVQ_CD];
     const int t = blockIdx.x, b = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const float* zr = z + ((size_t)b * T + t) * hidden;
     for (int c = tid; c < hidden; c += 256) sm[c] = zr[c];
     __syncthreads();

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(NT) void k_gemm(const bf16_t* __restrict__ A, long 
     const int n0 = blockIdx.x * BN * NTW, m0 = blockIdx.y * BM, split = blockIdx.z;
     const int kbeg = split * kslice;
     const int nchunks = kslice / BK;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ln = lane & 15, lg = lane >> 4;
 
     // this lane's weight rows (one per 16-column tile of the wave)
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
     const int n0 = bx * BNW, split = bz;
     const int kbeg = split * kslice;
     const int nchunks = kslice / BK;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ln = lane & 15, lg = lane >> 4;
 
     if (w >= NCW) {
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
                                                     const int32_t* skip) {
     __shared__ __attribute__((aligned(16))) f32x4 red[4][NTW][64];
     if (skip && *skip) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int split = blockIdx.z;
     const int nt0 = blockIdx.x * NTW;                          // first 16-column tile
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     __shared__ __attribute__((aligned(16))) uint4 xs[XS ? XR * GF_XS / 8 : 1];
     __shared__ __attribute__((aligned(16))) f32x4 red[NW][NTW][64];
     if (skip && *skip) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int nt0 = HALF ? (blockIdx.x >> 1) : blockIdx.x * NTW;    // first 16-column tile
     const int half = HALF ? (blockIdx.x & 1) : 0;

@@ -134,7 +134,7 @@ ZK_DEV int block_argmax(const float* x, int V, Smem& s) {
         const int oi = __shfl_xor(bi, o, 64);
         if (before(ov, oi, bv, bi)) { bv = ov; bi = oi; }
     }
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) { s.red[w] = bv; s.ired[w] = bi; }
     __syncthreads();
@@ -156,7 +156,7 @@ ZK_DEV void top_p_filter(float* p, int V, float top_p, Smem& s) {
 #pragma unroll
     for (int j = 0; j < SEG; ++j) if (base + j < V) loc += (double)s.key[base + j];
     // exclusive scan of `loc` over the block
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double inc = loc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
