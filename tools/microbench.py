@@ -62,6 +62,45 @@ def gemm():
         del Ws
 
 
+def warm():
+    """Experiment: k_gemm_ws launches whose first weight chunks were just read into L2 by a small
+    preceding kernel (zk_l2_warm_gemm) vs cold; time(pair) - time(warm kernel alone) vs time(cold)."""
+    M = 128
+    lib = _lib.load()
+    lib.zk_l2_warm_gemm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    for name, N, K, mode, ns in (("qkv", 3072, 2048, 0, 4), ("o", 2048, 2048, 0, 4), ("fc1", 16384, 2048, 1, 1),
+                                 ("fc2", 2048, 8192, 0, 8)):
+        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
+        Npad = (N + 63) // 64 * 64
+        Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        part = torch.empty(ns * M * N, device=dev)
+        out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
+        for chunks in (2, 4):
+            for nwg in (128, 256):
+                it = [0]
+
+                def g():
+                    W = Ws[it[0] % ncopy]; it[0] += 1
+                    call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, ns, mode, ptr(part), ptr(out), None, S)
+
+                def wg():
+                    W = Ws[it[0] % ncopy]; it[0] += 1
+                    rc = lib.zk_l2_warm_gemm(ptr(W), N, K, ns, chunks, nwg, ptr(sink), S)
+                    assert rc == 0
+
+                def pair():
+                    W = Ws[it[0] % ncopy]; it[0] += 1
+                    rc = lib.zk_l2_warm_gemm(ptr(W), N, K, ns, chunks, nwg, ptr(sink), S)
+                    assert rc == 0
+                    call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, ns, mode, ptr(part), ptr(out), None, S)
+                tc, tw, tp = timeit(g), timeit(wg), timeit(pair)
+                print(f"warm {name:4s} split={ns} chunks={chunks} nwg={nwg}: cold {tc:6.2f} us, warm kernel {tw:5.2f}, "
+                      f"pair {tp:6.2f} -> gemm after warm-up {tp - tw:6.2f} us", flush=True)
+        del Ws
+
+
 def prefill():
     """Prefill GEMMs at c3 (M = 2B x (Lc + P + 1) = 128 x 411 rows, split-K 1)."""
     M = 128 * 411
@@ -301,6 +340,8 @@ def dac():
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what == "warm":
+        warm()
     if what in ("gemm", "all"):
         gemm()
     if what in ("mamba",):

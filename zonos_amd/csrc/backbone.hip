@@ -14,6 +14,7 @@
 #include "common.h"
 #include "attn_common.h"
 #include "../../include/zonos_hip.h"
+#include "warm.h"
 #include <algorithm>
 #include <stdlib.h>
 
@@ -224,14 +225,25 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
 // the row, so every fp32 slab load instruction of a wave reads 1 KB contiguous; all slab loads of
 // a row are issued before the first add (one memory round trip); LayerNorm sums over 8 waves.
 // NS > 0: exactly NS slabs (only real slabs loaded); NS = 0: nsplit <= RL_MAXS with clamped loads
-template <int NS>
-__global__ __launch_bounds__(512) void k_resid_ln_d2k512(const float* part, int nsplit, const bf16_t* x_in,
+// WARM: a ninth wave warms the next GEMM's first weight chunks into L2 (warm.h) and keeps the
+// block's barrier count (two per row) without waiting for its loads.
+template <int NS, bool WARM = false>
+__global__ __launch_bounds__(WARM ? 576 : 512) void k_resid_ln_d2k512(const float* part, int nsplit, const bf16_t* x_in,
                                                          const bf16_t* w, const bf16_t* b, float eps, int rows,
                                                          bf16_t* x_out, bf16_t* xn_out, int ln_on_sum,
-                                                         const int32_t* skip) {
+                                                         const int32_t* skip, const bf16_t* wW, int wK, int wgx,
+                                                         int wgz, int wch) {
     constexpr int D = 2048;
     __shared__ float red[16];
     if (skip && *skip) return;
+    if (WARM && threadIdx.x >= 512) {
+        __shared__ __attribute__((aligned(16))) char sink[1024];
+        warm_units(wW, wK, wgx, wgz, wch, blockIdx.x, gridDim.x, 0, 1, threadIdx.x & 63, sink);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
     const int row = blockIdx.x, t = threadIdx.x;
     const size_t slab = (size_t)rows * D;
     const int c0 = 4 * t;
@@ -497,16 +509,28 @@ extern "C" int zk_layernorm(const void* x, const void* w, const void* b, float e
 extern "C" int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, const void* b, float eps,
                            int rows, int D, void* x_out, void* xn_out, int ln_on_sum, const int32_t* skip,
                            void* stream) {
+    return zk_resid_ln_warm(part, nsplit, x_in, w, b, eps, rows, D, x_out, xn_out, ln_on_sum, skip,
+                            ZkWarm{nullptr, 0, 0, 0, 0}, stream);
+}
+
+int zk_resid_ln_warm(const float* part, int nsplit, const void* x_in, const void* w, const void* b, float eps,
+                     int rows, int D, void* x_out, void* xn_out, int ln_on_sum, const int32_t* skip, ZkWarm warm,
+                     void* stream) {
     ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_resid_ln: unsupported D=%d", D);
     ZK_REQUIRE(nsplit >= 1, "zk_resid_ln: nsplit must be >= 1");
     if (rows == 0) return 0;
     // D = 2048: 512-thread rows (8 slabs 4.27 vs 4.41 us with 256 threads x 2 pieces, c3 decode
     // step 3.635 vs 3.646 ms, profiles/r2_s4_resid_ln_512_ab.txt)
     if (D == 2048 && nsplit <= RL_MAXS) {
-        auto kern = nsplit == 4 ? k_resid_ln_d2k512<4> : nsplit == 8 ? k_resid_ln_d2k512<8> : k_resid_ln_d2k512<0>;
-        hipLaunchKernelGGL(kern, dim3(rows), dim3(512), 0, (hipStream_t)stream, part, nsplit, (const bf16_t*)x_in,
-                           (const bf16_t*)w, (const bf16_t*)b, eps, rows, (bf16_t*)x_out, (bf16_t*)xn_out, ln_on_sum,
-                           skip);
+        // the warm-up wave needs rows % 8 == 0 to keep each GEMM workgroup's chunks on its own XCD
+        const bool wm = warm.W != nullptr && rows % 8 == 0;
+        auto kern = wm ? (nsplit == 4 ? k_resid_ln_d2k512<4, true> : nsplit == 8 ? k_resid_ln_d2k512<8, true>
+                                                                                : k_resid_ln_d2k512<0, true>)
+                       : (nsplit == 4 ? k_resid_ln_d2k512<4> : nsplit == 8 ? k_resid_ln_d2k512<8> : k_resid_ln_d2k512<0>);
+        hipLaunchKernelGGL(kern, dim3(rows), dim3(wm ? 576 : 512), 0, (hipStream_t)stream, part, nsplit,
+                           (const bf16_t*)x_in, (const bf16_t*)w, (const bf16_t*)b, eps, rows, (bf16_t*)x_out,
+                           (bf16_t*)xn_out, ln_on_sum, skip, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz,
+                           warm.chunks);
         ZK_CHECK_LAUNCH("zk_resid_ln");
         return 0;
     }

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/zonos_hip.h"
+#include "warm.h"
 
 static thread_local char g_err[1024] = "";
 
@@ -123,6 +124,15 @@ extern "C" int zk_event_destroy(void* ev) {
         if ((call) != 0) return -1;    \
     } while (0)
 
+// L2 warm-up descriptor of the decode GEMM zk_gemm_bf16(M, N, K, nsplit) (2 chunks per wave:
+// profiles/r3_l2_warm_micro.txt); ZK_L2_WARM=0 builds the step without it (A/B)
+#ifndef ZK_L2_WARM
+#define ZK_L2_WARM 1
+#endif
+static ZkWarm warm_desc(const void* W, int M, int N, int K, int nsplit) {
+    return ZK_L2_WARM ? zk_gemm_warm_desc(W, M, N, K, nsplit, 2) : ZkWarm{nullptr, 0, 0, 0, 0};
+}
+
 extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
     if (d == nullptr || d->layers == nullptr || d->n_layer <= 0 || d->B <= 0) {
         zk_set_error("zk_decode_step: bad descriptor");
@@ -166,14 +176,18 @@ extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
                                           d->smax, 1, pos, d->attn_work, d->attn_splits, d->attn_cnt, d->y,
                                           d->rope_neox, skip, stream));
             ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, R, D, H * hd, d->split_o, 0, d->part, nullptr, skip, stream));
-            ZK_STEP(zk_resid_ln(d->part, d->split_o, d->x, L.ln2_w, L.ln2_b, d->eps, R, D, d->x, d->xn, 0, skip,
-                                stream));
-            ZK_STEP(zk_gemm_bf16(d->xn, D, L.fc1, R, 2 * Fd, D, 1, 1, nullptr, d->h, skip, stream));
+            // each k_resid_ln and the fc1 GEMM warm the next GEMM's first weight chunks into L2 (warm.h)
+            ZK_STEP(zk_resid_ln_warm(d->part, d->split_o, d->x, L.ln2_w, L.ln2_b, d->eps, R, D, d->x, d->xn, 0, skip,
+                                     warm_desc(L.fc1, R, 2 * Fd, D, 1), stream));
+            ZK_STEP(zk_gemm_bf16_warm(d->xn, D, L.fc1, R, 2 * Fd, D, 1, 1, nullptr, d->h, skip,
+                                      warm_desc(L.fc2, R, D, Fd, d->split_fc2), stream));
             ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, R, D, Fd, d->split_fc2, 0, d->part, nullptr, skip, stream));
             const bool last = i + 1 == d->n_layer;
-            ZK_STEP(zk_resid_ln(d->part, d->split_fc2, d->x, last ? d->lnf_w : d->layers[i + 1].ln1_w,
-                                last ? d->lnf_b : d->layers[i + 1].ln1_b, d->eps, R, D, d->x, d->xn, 0, skip,
-                                stream));
+            const ZkWarm next = last ? warm_desc(d->heads, R, K * V, D, d->split_heads)
+                                     : warm_desc(d->layers[i + 1].wqkv, R, Nqkv, D, d->split_qkv);
+            ZK_STEP(zk_resid_ln_warm(d->part, d->split_fc2, d->x, last ? d->lnf_w : d->layers[i + 1].ln1_w,
+                                     last ? d->lnf_b : d->layers[i + 1].ln1_b, d->eps, R, D, d->x, d->xn, 0, skip,
+                                     next, stream));
         }
     }
     // 9 heads (model.py:104-111): small path with norm_f as the GEMV prologue, one slab
@@ -251,6 +265,15 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
     const int32_t* pos = prefill ? nullptr : scal + 1;
     const int sq = prefill ? 1 : d->split_qkv, so = prefill ? 1 : d->split_o, sf = prefill ? 1 : d->split_fc2;
     const int si = prefill ? 1 : d->split_inp, su = prefill ? 1 : d->split_out;
+    const int K = d->st.K, V = d->st.V;
+    // L2 warm-up (warm.h) of the GEMM that follows layer i's last k_resid_ln: the next layer's first
+    // GEMM, or the heads
+    auto next_warm = [&](int i) {
+        if (prefill) return ZkWarm{nullptr, 0, 0, 0, 0};
+        if (i + 1 == d->n_layer) return warm_desc(d->heads, M, K * V, D, d->split_heads);
+        const zk_hybrid_layer& N1 = d->layers[i + 1];
+        return N1.type == 0 ? warm_desc(N1.wqkv, M, Nqkv, D, sq) : warm_desc(N1.w_in, M, nin, D, si);
+    };
     for (int i = 0; i < d->n_layer; ++i) {
         const zk_hybrid_layer& L = d->layers[i];
         const bool last = i + 1 == d->n_layer;
@@ -267,10 +290,13 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
                                            pos, d->attn_work, d->attn_splits, d->y, 1, skip, stream));
             }
             ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, M, D, H * hd, so, 0, d->part, nullptr, skip, stream));
-            ZK_STEP(zk_resid_ln(d->part, so, d->x, L.ln2_w, L.ln2_b, d->eps, M, D, d->x, d->xn, 1, skip, stream));
-            ZK_STEP(zk_gemm_bf16(d->xn, D, L.fc1, M, 2 * Fd, D, 1, 1, nullptr, d->h, skip, stream));
+            ZK_STEP(zk_resid_ln_warm(d->part, so, d->x, L.ln2_w, L.ln2_b, d->eps, M, D, d->x, d->xn, 1, skip,
+                                     prefill ? ZkWarm{nullptr, 0, 0, 0, 0} : warm_desc(L.fc1, M, 2 * Fd, D, 1), stream));
+            ZK_STEP(zk_gemm_bf16_warm(d->xn, D, L.fc1, M, 2 * Fd, D, 1, 1, nullptr, d->h, skip,
+                                      prefill ? ZkWarm{nullptr, 0, 0, 0, 0} : warm_desc(L.fc2, M, D, Fd, sf), stream));
             ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, M, D, Fd, sf, 0, d->part, nullptr, skip, stream));
-            ZK_STEP(zk_resid_ln(d->part, sf, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, stream));
+            ZK_STEP(zk_resid_ln_warm(d->part, sf, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, next_warm(i),
+                                     stream));
         } else if (L.type == 1) {
             ZK_STEP(zk_gemm_bf16(d->xn, D, L.w_in, M, nin, D, si, 0, d->part, nullptr, skip, stream));
             if (prefill) {
@@ -285,7 +311,8 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
             }
             ZK_STEP(zk_gated_rmsnorm(d->yz, M, di, L.norm_w, d->gate_eps, d->ym, skip, stream));
             ZK_STEP(zk_gemm_bf16(d->ym, di, L.w_out, M, D, di, su, 0, d->part, nullptr, skip, stream));
-            ZK_STEP(zk_resid_ln(d->part, su, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, stream));
+            ZK_STEP(zk_resid_ln_warm(d->part, su, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, next_warm(i),
+                                     stream));
         } else {
             zk_set_error("zk_hybrid: layer %d has unknown type %d", i, L.type);
             return -1;

@@ -33,6 +33,56 @@ ZK_DEV uint4 pack8(const float* f) {
     return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// ---------------------------------------------------------------- decode GEMM tile order
+#ifndef ZK_WS_XCD
+#define ZK_WS_XCD 1                // k_gemm_ws: XCD-aware split-major tile order
+#endif
+// Tile (bx, bz) of linear workgroup id L (= blockIdx.x + gx * blockIdx.z) of a k_gemm_ws grid
+// gx x 1 x gz. XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (L % 8),
+// and every workgroup of one K split reads the same activation slice. Numbering the work
+// split-major and handing each XCD a contiguous run of it puts one split (fc2: 8 splits) or half a
+// split (in_proj / out_proj: 4) on each XCD, so its L2 fetches only that K slice of the activation
+// instead of all of it. Placement only: every tile computes the same numbers.
+ZK_DEV void ws_tile(int L, int gx, int gz, int& bx, int& bz) {
+    if (ZK_WS_XCD && gz > 1 && ((gx * gz) & 7) == 0) {
+        const int I = (L & 7) * ((gx * gz) >> 3) + (L >> 3);
+        bz = I / gx;
+        bx = I - bz * gx;
+    } else {
+        bz = L / gx;
+        bx = L - bz * gx;
+    }
+}
+
+// L2 warm-up (warm.h): compute wave w of k_gemm_ws workgroup L starts by streaming its first
+// `chunks` 2 KB chunks of fragment-packed weights ([N/16][K/32][64 lanes][8]: 16 rows x 64 k =
+// 2 KB). Issue them as LDS-DMA (default cache policy, so the lines stay in this XCD's L2) into a
+// 1 KB LDS sink the issuing wave never reads: no registers, nothing for the other waves to wait on.
+// Returns the number of loads issued (2 per chunk).
+ZK_DEV int warm_unit(const bf16_t* W, int K, int gx, int gz, int chunks, int L, int w, int lane, void* sink) {
+    int bx, bz;
+    ws_tile(L, gx, gz, bx, bz);
+    const int kbeg = bz * (K / gz);
+    const bf16_t* p = W + ((size_t)(bx * 4 + w) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
+    for (int c = 0; c < chunks; ++c) {
+        __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024), sink, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024 + 512), sink, 16, 0, 0);
+    }
+    return 2 * chunks;
+}
+
+// All warm-up units of workgroup r of an nwg-workgroup launch (nwg % 8 == 0 keeps the GEMM
+// workgroups L = r, r + nwg, ... on r's XCD), unit u = (GEMM workgroup, compute wave), this wave
+// taking units first, first + step, ...
+ZK_DEV void warm_units(const bf16_t* W, int K, int gx, int gz, int chunks, int r, int nwg, int first, int step,
+                       int lane, void* sink) {
+    for (int u = first;; u += step) {
+        const int L = r + (u >> 2) * nwg;
+        if (L >= gx * gz) break;
+        warm_unit(W, K, gx, gz, chunks, L, u & 3, lane, sink);
+    }
+}
+
 // ---------------------------------------------------------------- wave64 reductions
 ZK_DEV float wave_sum(float v) {
 #pragma unroll

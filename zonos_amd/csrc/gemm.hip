@@ -20,6 +20,7 @@
 #include "common.h"
 #include "attn_common.h"
 #include "../../include/zonos_hip.h"
+#include "warm.h"
 #include <algorithm>
 #include <stdlib.h>
 
@@ -251,9 +252,6 @@ constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 #ifndef ZK_SLAB_SC1
 #define ZK_SLAB_SC1 0              // write-through (sc1) slab stores: nothing left dirty in L2 at the boundary
 #endif
-#ifndef ZK_WS_XCD
-#define ZK_WS_XCD 1                // k_gemm_ws: XCD-aware split-major tile order
-#endif
 #ifndef ZK_WS_EPI
 #define ZK_WS_EPI 1                // k_gemm_ws epilogue staged through LDS (whole-row stores)
 #endif
@@ -271,23 +269,13 @@ template <int MODE, int NCH, int PF, int MT, int NCW = 4>
 __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
-                                                           bf16_t* __restrict__ Cout, const int32_t* skip) {
+                                                           bf16_t* __restrict__ Cout, const int32_t* skip,
+                                                           const bf16_t* __restrict__ wW, int wK, int wgx, int wgz,
+                                                           int wch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip && *skip) return;
-    int bx = blockIdx.x, bz = blockIdx.z;
-#if ZK_WS_XCD
-    // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (linear id % 8),
-    // and every workgroup of one K split reads the same activation slice. Numbering the work
-    // split-major and handing each XCD a contiguous run of it puts one split (fc2: 8 splits) or
-    // half a split (in_proj / out_proj: 4) on each XCD, so its L2 fetches only that K slice of the
-    // activation instead of all of it. Placement only: every tile computes the same numbers.
-    if (gridDim.z > 1 && ((gridDim.x * gridDim.z) & 7) == 0) {
-        const int L = blockIdx.x + gridDim.x * blockIdx.z;               // gridDim.y == 1
-        const int I = (L & 7) * ((gridDim.x * gridDim.z) >> 3) + (L >> 3);
-        bz = I / gridDim.x;
-        bx = I - bz * gridDim.x;
-    }
-#endif
+    int bx, bz;
+    ws_tile(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x, gridDim.z, bx, bz);     // gridDim.y == 1
     constexpr int BNW = 16 * NCW;                 // columns per workgroup (16 per compute wave)
     const int n0 = bx * BNW, split = bz;
     const int kbeg = split * kslice;
@@ -334,6 +322,19 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
             __builtin_amdgcn_s_barrier();                           // publish chunk `need`
             asm volatile("" ::: "memory");
             if (c + WS_DA < nchunks) issue(c + WS_DA);              // its slot was read >= 2 chunks ago
+        }
+        if (wW != nullptr) {
+            // L2 warm-up of the NEXT GEMM (warm.h): its workgroups L, L + nwg, ... run on this XCD;
+            // the loaders, idle from here on, stream their compute waves' first chunks into L2 (LDS-DMA
+            // into the 1 KB sink past the ring), then keep the workgroup's barrier count: the epilogue's
+            // two __syncthreads must not wait for these loads
+            warm_units(wW, wK, wgx, wgz, wch, blockIdx.x + gridDim.x * blockIdx.z, gridDim.x * gridDim.z, ld, WS_NLD,
+                       lane, smem + WS_NB * (MT * 16 * BK * 2));
+            if (ZK_WS_EPI && (MODE == 1 || N % 4 == 0)) {
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_s_barrier();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         return;
     }
@@ -895,8 +896,30 @@ extern "C" int zk_pack_weights(const void* w, int N, int K, void* out, void* str
     return 0;
 }
 
+#ifndef ZK_WS_NCW
+#define ZK_WS_NCW 4                // k_gemm_ws compute waves (16-column tiles) per workgroup
+#endif
+
+// k_gemm_ws regime of zk_gemm_bf16_warm below (16 < M <= 128 or M <= 16 with K/nsplit % 128 != 0)
+static bool ws_regime(int M, int K, int nsplit) {
+    if (M <= 16 && (K / nsplit) % 128 == 0) return false;
+    return M <= BM && K / nsplit / BK <= 32;
+}
+
+ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int chunks) {
+    if (W == nullptr || M <= 16 || ZK_WS_NCW != 4 || !ws_regime(M, K, nsplit) || K % (nsplit * BK) != 0)
+        return ZkWarm{nullptr, 0, 0, 0, 0};
+    return ZkWarm{W, K, (N + BN - 1) / BN, nsplit, std::min(chunks, K / nsplit / BK)};
+}
+
 extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
                             float* Cpart, void* Cout, const int32_t* skip_flag, void* stream) {
+    return zk_gemm_bf16_warm(A, lda, W, M, N, K, nsplit, mode, Cpart, Cout, skip_flag, ZkWarm{nullptr, 0, 0, 0, 0},
+                             stream);
+}
+
+int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
+                      float* Cpart, void* Cout, const int32_t* skip_flag, ZkWarm warm, void* stream) {
     ZK_REQUIRE(M > 0 && N > 0 && K > 0, "zk_gemm_bf16: empty shape M=%d N=%d K=%d", M, N, K);
     ZK_REQUIRE(nsplit >= 1 && K % (nsplit * BK) == 0, "zk_gemm_bf16: K=%d must be a multiple of nsplit*%d", K, BK);
     ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemm_bf16: lda=%ld", lda);
@@ -939,13 +962,10 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
         }
     }
     if (M <= BM && nchunks <= 32) {
-#ifndef ZK_WS_NCW
-#define ZK_WS_NCW 4
-#endif
         constexpr int NCW = ZK_WS_NCW;            // compute waves = 16-column tiles per workgroup
         dim3 g((N + 16 * NCW - 1) / (16 * NCW), 1, nsplit);
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
-        const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2;
+        const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2 + (warm.W ? 1024 : 0);     // + warm-up sink
 #define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
     do {                                                                                                          \
         if (lds > 65536)                                                                                          \
@@ -954,7 +974,7 @@ extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N
         hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, WS_PF, MT_, NCW>), g, dim3(64 * (NCW + WS_NLD)), lds,          \
                            (hipStream_t)stream,                                                                   \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
-                           skip_flag);                                                                             \
+                           skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks);              \
         handled = true;                                                                                           \
     } while (0)
 #define ZK_WS_LAUNCH(MODE_, NCH_)                                                                                  \
@@ -1113,6 +1133,27 @@ extern "C" int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const vo
     }
 #undef ZK_GAO
     ZK_CHECK_LAUNCH("zk_gemv_attn_out");
+    return 0;
+}
+
+// L2 warm-up of a k_gemm_ws launch's first weight chunks (experiment): workgroup r of a 1-D grid
+// (same XCD as r % 8) reads, for every GEMM workgroup L = r, r + nwg, ... (same XCD), the first
+// `chunks` 2 KB weight chunks of each of its 4 compute waves, so they are L2 hits when it starts.
+__global__ __launch_bounds__(256) void k_l2_warm_ws(const bf16_t* __restrict__ W, int K, int gx, int gz, int chunks,
+                                                    uint32_t* sink) {
+    __shared__ __attribute__((aligned(16))) char lsink[1024];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    warm_units(W, K, gx, gz, chunks, blockIdx.x, gridDim.x, w, 4, lane, lsink);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    (void)sink;
+}
+
+extern "C" int zk_l2_warm_gemm(const void* W, int N, int K, int nsplit, int chunks, int nwg, void* sink, void* stream) {
+    ZK_REQUIRE(N > 0 && K % (nsplit * BK) == 0 && chunks >= 1 && chunks <= K / nsplit / BK && nwg > 0,
+               "zk_l2_warm_gemm: N=%d K=%d nsplit=%d chunks=%d", N, K, nsplit, chunks);
+    hipLaunchKernelGGL(k_l2_warm_ws, dim3(nwg), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)W, K,
+                       (N + BN - 1) / BN, nsplit, chunks, (uint32_t*)sink);
+    ZK_CHECK_LAUNCH("zk_l2_warm_gemm");
     return 0;
 }
 
