@@ -81,6 +81,17 @@ ZK_DEV void wait_vm(int n) {
 #ifndef ZK_CL_DA
 #define ZK_CL_DA 3
 #endif
+#ifdef ZK_CL_PROF                  // diagnostic builds only: per-step s_memtime stamps of 64 workgroups
+__device__ uint64_t g_clprof[64][3][64];   // [wg][0: loader before wait, 1: loader after barrier, 2: compute after barrier][step]
+__device__ uint64_t g_clprof_end[64][2];   // compute wave: after the MFMAs of the last step, at the end
+__device__ uint64_t g_clprof_rt[64][6];    // wave 0: realtime at start, first barrier, loop end, epilogue end; memtime at start, end
+#define ZK_CL_STAMP(role, st)                                                                          \
+    do {                                                                                               \
+        if (blockIdx.x < 64 && (st) < 64 && lane == 0) g_clprof[blockIdx.x][role][st] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define ZK_CL_STAMP(role, st) do { } while (0)
+#endif
 #ifndef ZK_CL_DIAG_NOW             // diagnostic builds only: weight slices loaded once (stale data)
 #define ZK_CL_DIAG_NOW 0
 #endif
@@ -138,6 +149,12 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
     char* const xring = smem + (DA + 2) * WS;
     const int nchunk = Cin / CI, nstep = nchunk * ks;
 
+#ifdef ZK_CL_PROF
+    if (wv == 0 && blockIdx.x < 64 && lane == 0) {
+        g_clprof_rt[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+        g_clprof_rt[blockIdx.x][4] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     if (wv >= 4) {
         // ---------------- loader waves: loader lw moves the pieces p with p % CL_NLD == lw
         // wave-uniform (readfirstlane): the piece counts and the vmcnt switch below stay scalar;
@@ -145,58 +162,68 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
         // chain of exec-masked branches (the loader then paced every step: convs +20 %)
         const int lw = __builtin_amdgcn_readfirstlane(wv - 4);
         const int len_in = lens ? min(lens[b] * in_scale, Tin) : Tin;
-        const uint16_t* wp = w + (size_t)phase * wphase;
         const size_t wtap = (size_t)Cout * Cin;
-        const uint16_t* inb = in + (size_t)b * Tin * Cin;
         const int u0 = q0 - pad;
-        const int prow = lane >> 2, pslot = lane & 3;   // a 1 KiB piece = 16 rows x 4 slots
+        // A 1 KiB piece = 16 rows x 4 16-B slots; lane -> (row prow, slot pslot). With CI = 32 the
+        // image swizzle of row p*16 + prow does not depend on the piece p, so this lane's source
+        // offset inside any piece is one constant: no per-piece index math on the loader's path
+        // (the per-step divisions and 64-bit address arithmetic of the plain form made the loader,
+        // not the MFMAs, pace every step).
+        static_assert((16 / I::RPB) % I::G == 0, "piece-invariant swizzle needs 16-row pieces to span whole swizzle periods");
+        const int prow = lane >> 2, pslot = lane & 3;
+        const int g = pslot ^ I::swz(prow);
+        const int loff = prow * Cin + g * 8;
+        const long prs = 16L * Cin;                                  // elements per 16-row piece
+        const uint16_t* xsrc0 = in + (size_t)b * Tin * Cin + loff + (long)u0 * Cin;   // row u0 of the window
+        const uint16_t* wsrc0 = w + (size_t)phase * wphase + (size_t)co0 * Cin + loff;
+        // every window row inside [0, len_in): no per-lane range checks (rows past `win` are read but unused)
+        const bool xfast = u0 >= 0 && u0 + nxp * 16 <= len_in;
+        const int nxl = (nxp - lw + CL_NLD - 1) / CL_NLD, nwl = (NWP - lw + CL_NLD - 1) / CL_NLD;
         int hist[DA + 1] = {};                       // loads issued by iterations j-DA .. j
+        int tx = 0, cx = 0, xslot = 0;               // window stream at sx = j + dx: tap, chunk, ring slot
+        int tw = 0, cw = 0, wslot = 0;               // weight stream at sw = j + DA (once sw >= 0)
         for (int j = -dx; j < nstep; ++j) {
             int nl = 0;
             // window first: a window issued in the same iteration as W(j+DA) is then older
             // than it, so waiting for W(j) below also covers every window step j can need
             const int sx = j + dx;
-            if (sx >= 0 && sx < nstep && sx % ks == 0) {
-                const int c = sx / ks;
-                char* dst = xring + (c % nx_slots) * XS;
-                for (int p = lw; p < nxp; p += CL_NLD) {
-                    const int row = p * 16 + prow;
-                    const int u = u0 + row;
-                    const int g = pslot ^ I::swz(row);
-                    const void* src = (row < win && u >= 0 && u < len_in)
-                                          ? (const void*)(inb + (size_t)u * Cin + c * CI + g * 8)
-                                          : (const void*)g_zero_page;
-                    __builtin_amdgcn_global_load_lds(src, (void*)(dst + p * 1024), 16, 0, 0);
+            if (sx < nstep) {
+                if (tx == 0) {
+                    char* dst = xring + xslot * XS;
+                    const uint16_t* src = xsrc0 + cx * CI;
+                    if (xfast) {
+                        for (int p = lw; p < nxp; p += CL_NLD)
+                            __builtin_amdgcn_global_load_lds((const void*)(src + p * prs), (void*)(dst + p * 1024), 16,
+                                                             0, 0);
+                    } else {
+                        for (int p = lw; p < nxp; p += CL_NLD) {
+                            const int row = p * 16 + prow, u = u0 + row;
+                            const void* sp = (row < win && u >= 0 && u < len_in) ? (const void*)(src + p * prs)
+                                                                                 : (const void*)g_zero_page;
+                            __builtin_amdgcn_global_load_lds(sp, (void*)(dst + p * 1024), 16, 0, 0);
+                        }
+                    }
+                    nl += nxl;
+                    if (++xslot == nx_slots) xslot = 0;
                 }
-                nl += (nxp - lw + CL_NLD - 1) / CL_NLD;
+                if (++tx == ks) { tx = 0; ++cx; }
             }
             const int sw = j + DA;
-            if (!ZK_CL_DIAG_NOW && sw >= 0 && sw < nstep) {
-                const int c = sw / ks, t = sw - c * ks;
-                char* dst = wring + (sw % (DA + 2)) * WS;
-                const uint16_t* src0 = wp + t * wtap + (size_t)co0 * Cin + c * CI;
+            if (sw >= 0 && sw < nstep) {
+                if (!ZK_CL_DIAG_NOW || sw < DA + 2) {     // (diag: each weight slot filled once)
+                    char* dst = wring + wslot * WS;
+                    const uint16_t* src = wsrc0 + tw * wtap + cw * CI;
 #pragma unroll
-                for (int pp = 0; pp < (NWP + CL_NLD - 1) / CL_NLD; ++pp) {
-                    const int p = pp * CL_NLD + lw;
-                    if (p >= NWP) break;
-                    const int row = p * 16 + prow;
-                    const int g = pslot ^ I::swz(row);
-                    __builtin_amdgcn_global_load_lds((const void*)(src0 + (size_t)row * Cin + g * 8),
-                                                     (void*)(dst + p * 1024), 16, 0, 0);
+                    for (int pp = 0; pp < (NWP + CL_NLD - 1) / CL_NLD; ++pp) {
+                        const int p = pp * CL_NLD + lw;
+                        if (p >= NWP) break;
+                        __builtin_amdgcn_global_load_lds((const void*)(src + p * prs), (void*)(dst + p * 1024), 16, 0,
+                                                         0);
+                    }
+                    nl += nwl;
                 }
-                nl += (NWP - lw + CL_NLD - 1) / CL_NLD;
-            }
-            if (ZK_CL_DIAG_NOW && sw >= 0 && sw < nstep && sw < DA + 2) {      // diag: fill each weight slot once
-                const int c = sw / ks, t = sw - c * ks;
-                char* dst = wring + (sw % (DA + 2)) * WS;
-                const uint16_t* src0 = wp + t * wtap + (size_t)co0 * Cin + c * CI;
-                for (int p = lw; p < NWP; p += CL_NLD) {
-                    const int row = p * 16 + prow;
-                    const int g = pslot ^ I::swz(row);
-                    __builtin_amdgcn_global_load_lds((const void*)(src0 + (size_t)row * Cin + g * 8),
-                                                     (void*)(dst + p * 1024), 16, 0, 0);
-                }
-                nl += (NWP - lw + CL_NLD - 1) / CL_NLD;
+                if (++wslot == DA + 2) wslot = 0;
+                if (++tw == ks) { tw = 0; ++cw; }
             }
 #pragma unroll
             for (int k = 0; k < DA; ++k) hist[k] = hist[k + 1];
@@ -206,8 +233,10 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
                 int pend = 0;
 #pragma unroll
                 for (int k = 1; k <= DA; ++k) pend += hist[k];
+                if (lw == 0) ZK_CL_STAMP(0, j);
                 wait_vm(pend);
                 __builtin_amdgcn_s_barrier();           // publish step j
+                if (lw == 0) ZK_CL_STAMP(1, j);
             }
         }
         return;
@@ -238,12 +267,17 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
             }
     }
 
+    int t = 0, xslot = 0, wslot = 0;             // tap, window ring slot, weight ring slot of step s
     for (int s = 0; s < nstep; ++s) {
-        const int c = s / ks, t = s - c * ks;
         __builtin_amdgcn_s_barrier();            // step s is in LDS
         asm volatile("" ::: "memory");
-        const char* xb = xring + (c % nx_slots) * XS;
-        const char* wb = wring + (s % (DA + 2)) * WS;
+        if (wv == 0) ZK_CL_STAMP(2, s);
+#ifdef ZK_CL_PROF
+        if (s == 0 && wv == 0 && blockIdx.x < 64 && lane == 0) g_clprof_rt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
+        const char* xb = xring + xslot * XS;
+        const char* wb = wring + wslot * WS;
+        if (++wslot == DA + 2) wslot = 0;
         uint4 a[FM], bq[NQ];
 #pragma unroll
         for (int m = 0; m < FM; ++m)
@@ -263,8 +297,23 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
                 for (int n = 0; n < NQ; ++n)
                     acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a[m]), as_h8(bq[n]), acc[m][n], 0, 0, 0);
         }
+        if (++t == ks) {
+            t = 0;
+            if (++xslot == nx_slots) xslot = 0;
+        }
     }
 
+#ifdef ZK_CL_PROF
+    if (wv == 0 && blockIdx.x < 64 && lane == 0) {
+        float keep = 0.f;
+#pragma unroll
+        for (int m = 0; m < FM; ++m)
+#pragma unroll
+            for (int n = 0; n < NQ; ++n) keep += acc[m][n][0];
+        g_clprof_end[blockIdx.x][0] = __builtin_amdgcn_s_memtime() + (keep == 1.2345f);
+        g_clprof_rt[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 16NQ wn + 16n + ln]
     const int len_out = lens ? lens[b] * out_scale : Tout;
     const int out_off = out_off0 + phase;
@@ -309,6 +358,13 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
                             snake_fast(v3, aa.w, r3));
         }
     }
+#ifdef ZK_CL_PROF
+    if (wv == 0 && blockIdx.x < 64 && lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        g_clprof_rt[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+        g_clprof_rt[blockIdx.x][5] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 // z[b][t][ch] = fp16(sum_k E_k[code_k][ch]) channels-last, zero beyond the row's length
@@ -606,6 +662,14 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     ZK_CHECK_LAUNCH("zk_dac_conv_cl");
     return 0;
 }
+
+#ifdef ZK_CL_PROF
+extern "C" int zk_cl_prof_read(void* dst, void* dst_end) {
+    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_clprof), sizeof(g_clprof)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(dst_end, HIP_SYMBOL(g_clprof_rt), sizeof(g_clprof_rt)) != hipSuccess) return -1;
+    return 0;
+}
+#endif
 
 extern "C" int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias, float* out,
                               const int32_t* lens, int scale, void* stream) {
