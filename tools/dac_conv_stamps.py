@@ -57,6 +57,23 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 5
 fm = 3 if Cc % 96 == 0 and Cc // 32 % 4 else 4
+wg = np.zeros((4096, 2), dtype=np.uint64)
+lib.zk_cl_prof_read_wg.argtypes = [C.c_void_p]
+assert lib.zk_cl_prof_read_wg(wg.ctypes.data) == 0
+wg = wg.astype(np.int64)
+nw = min(4096, int((wg[:, 0] > 0).sum()))
+st, en = wg[:nw, 0], wg[:nw, 1]
+t0 = st.min()
+ev = sorted([(t, 1) for t in st] + [(t, -1) for t in en])
+cur = best = 0
+act = []
+for t, d in ev:
+    cur += d
+    act.append((t, cur))
+best = max(a for _, a in act)
+tmid = t0 + (en.max() - t0) // 2
+print(f"  workgroups 0..{nw - 1}: resident at once max {best}, at mid-run {max(a for t, a in act if t <= tmid)}; "
+      f"median lifetime {np.median(en - st) / 100:.2f} us; first {nw} span {(en.max() - t0) / 100:.1f} us")
 print(f"  launch {ms * 1e3:.1f} us, {2 * Cc * Cc * ks * B * T / ms / 1e9:.0f} TFLOP/s")
 for s_ in (0, 1, 2, 6, 7, 8, 13, 14, 20, 21):
     if s_ + 1 < nstep:

@@ -85,6 +85,7 @@ ZK_DEV void wait_vm(int n) {
 __device__ uint64_t g_clprof[64][3][64];   // [wg][0: loader before wait, 1: loader after barrier, 2: compute after barrier][step]
 __device__ uint64_t g_clprof_end[64][2];   // compute wave: after the MFMAs of the last step, at the end
 __device__ uint64_t g_clprof_rt[64][6];    // wave 0: realtime at start, first barrier, loop end, epilogue end; memtime at start, end
+__device__ uint64_t g_clwg[4096][2];       // every workgroup < 4096: realtime at start / end of wave 0
 #define ZK_CL_STAMP(role, st)                                                                          \
     do {                                                                                               \
         if (blockIdx.x < 64 && (st) < 64 && lane == 0) g_clprof[blockIdx.x][role][st] = __builtin_amdgcn_s_memtime(); \
@@ -150,6 +151,7 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
     const int nchunk = Cin / CI, nstep = nchunk * ks;
 
 #ifdef ZK_CL_PROF
+    if (wv == 0 && blockIdx.x < 4096 && lane == 0) g_clwg[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
     if (wv == 0 && blockIdx.x < 64 && lane == 0) {
         g_clprof_rt[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
         g_clprof_rt[blockIdx.x][4] = __builtin_amdgcn_s_memtime();
@@ -250,6 +252,19 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
 #pragma unroll
         for (int n = 0; n < NQ; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // Epilogue constants of this workgroup's CO_T channels -- bias, Snake alpha, 1/(alpha + 1e-9) --
+    // staged into an LDS table while the loader fills the rings (the epilogue used to start with
+    // their global loads and four IEEE divisions per channel quartet)
+    float* const ept = reinterpret_cast<float*>(xring + nx_slots * XS);
+    for (int i = tid; i < CO_T; i += 256) {
+        const float a_ = sout ? alpha[co0 + i] : 1.f;
+        ept[i] = bias[co0 + i];
+        ept[CO_T + i] = a_;
+        ept[2 * CO_T + i] = __fdiv_rn(1.0f, __fadd_rn(a_, 1e-9f));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // visible after the first barrier
+    const int len_out = lens ? lens[b] * out_scale : Tout;
+
     // RES (resid != nullptr: the 1x1 convs of the residual units): the residual tile is loaded
     // before the main loop, so its latency overlaps the loader's first DMA instead of following
     // the last MFMA (clamped, unconditional loads; out-of-range positions are never stored).
@@ -315,15 +330,14 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
     }
 #endif
     // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 16NQ wn + 16n + ln]
-    const int len_out = lens ? lens[b] * out_scale : Tout;
     const int out_off = out_off0 + phase;
 #pragma unroll
     for (int m = 0; m < FM; ++m) {
-        const int co = co0 + wm * 16 * FM + m * 16 + lg * 4;
-        const float4 bb = *reinterpret_cast<const float4*>(bias + co);
-        const float4 aa = sout ? *reinterpret_cast<const float4*>(alpha + co) : make_float4(1.f, 1.f, 1.f, 1.f);
-        const float r0 = __fdiv_rn(1.0f, __fadd_rn(aa.x, 1e-9f)), r1 = __fdiv_rn(1.0f, __fadd_rn(aa.y, 1e-9f));
-        const float r2 = __fdiv_rn(1.0f, __fadd_rn(aa.z, 1e-9f)), r3 = __fdiv_rn(1.0f, __fadd_rn(aa.w, 1e-9f));
+        const int cl = wm * 16 * FM + m * 16 + lg * 4, co = co0 + cl;
+        const float4 bb = *reinterpret_cast<const float4*>(ept + cl);
+        const float4 aa = *reinterpret_cast<const float4*>(ept + CO_T + cl);
+        const float4 rr = *reinterpret_cast<const float4*>(ept + 2 * CO_T + cl);
+        const float r0 = rr.x, r1 = rr.y, r2 = rr.z, r3 = rr.w;
 #pragma unroll
         for (int n = 0; n < NQ; ++n) {
             const int q = q0 + wn * 16 * NQ + n * 16 + ln;
@@ -359,6 +373,10 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
         }
     }
 #ifdef ZK_CL_PROF
+    if (wv == 0 && blockIdx.x < 4096 && lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        g_clwg[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (wv == 0 && blockIdx.x < 64 && lane == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         g_clprof_rt[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
@@ -637,12 +655,13 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     const int da = CL_DA;
     const size_t lds_cap = 80 * 1024;
     // window lead DX >= da steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
+    const size_t ept = (size_t)3 * 32 * FM * sizeof(float);          // epilogue constants table
     int dx = std::max(da, ks), nx = 1 + (dx + 1 + ks - 1) / ks;
-    while (dx > da && (da + 2) * ws + nx * xs > lds_cap) {
+    while (dx > da && (da + 2) * ws + nx * xs + ept > lds_cap) {
         --dx;
         nx = 1 + (dx + 1 + ks - 1) / ks;
     }
-    const size_t lds = (da + 2) * ws + nx * xs;
+    const size_t lds = (da + 2) * ws + nx * xs + ept;
     ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_conv_cl: LDS %zu too large", lds);
     const int nq = (Qn + qt - 1) / qt;
     const long nwg = (long)B * nq * (Cout / (32 * FM)) * nphase;
@@ -668,6 +687,9 @@ extern "C" int zk_cl_prof_read(void* dst, void* dst_end) {
     if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_clprof), sizeof(g_clprof)) != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(dst_end, HIP_SYMBOL(g_clprof_rt), sizeof(g_clprof_rt)) != hipSuccess) return -1;
     return 0;
+}
+extern "C" int zk_cl_prof_read_wg(void* dst) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_clwg), sizeof(g_clwg)) == hipSuccess ? 0 : -1;
 }
 #endif
 
