@@ -74,6 +74,23 @@ best = max(a for _, a in act)
 tmid = t0 + (en.max() - t0) // 2
 print(f"  workgroups 0..{nw - 1}: resident at once max {best}, at mid-run {max(a for t, a in act if t <= tmid)}; "
       f"median lifetime {np.median(en - st) / 100:.2f} us; first {nw} span {(en.max() - t0) / 100:.1f} us")
+hw = np.zeros((4096, 8), dtype=np.uint32)
+lib.zk_cl_prof_read_hw.argtypes = [C.c_void_p]
+assert lib.zk_cl_prof_read_hw(hw.ctypes.data) == 0
+hw = hw[:nw].astype(np.int64)
+cu_key = (hw[:, 6] << 16) | (((hw[:, 0] >> 13) & 7) << 8) | (((hw[:, 0] >> 12) & 1) << 4) | ((hw[:, 0] >> 8) & 15)
+from collections import Counter
+per_cu = Counter(cu_key.tolist())
+print(f"  CUs used {len(per_cu)}, workgroups per CU: {sorted(Counter(per_cu.values()).items())}")
+simd = (hw[:, :6] >> 4) & 3
+pat = Counter(tuple(np.bincount(simd[i], minlength=4).tolist()) for i in range(nw))
+print(f"  waves per SIMD within a workgroup (waves 0-5): {pat.most_common(4)}")
+# concurrent pairs on one CU: SIMD totals
+tot = {}
+for i in range(nw):
+    tot.setdefault(int(cu_key[i]), np.zeros(4, dtype=int))
+    tot[int(cu_key[i])] += np.bincount(simd[i], minlength=4)
+print(f"  per-CU SIMD wave totals (all its workgroups): {Counter(tuple(v.tolist()) for v in tot.values()).most_common(5)}")
 print(f"  launch {ms * 1e3:.1f} us, {2 * Cc * Cc * ks * B * T / ms / 1e9:.0f} TFLOP/s")
 for s_ in (0, 1, 2, 6, 7, 8, 13, 14, 20, 21):
     if s_ + 1 < nstep:

@@ -175,3 +175,18 @@ extern "C" void zk_set_error(const char* fmt, ...);
             return -2;                  \
         }                               \
     } while (0)
+// a HIP runtime call that must succeed (host code returning int status)
+#define ZK_HIP(call)                                                                   \
+    do {                                                                               \
+        hipError_t _e = (call);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            zk_set_error("%s failed: %s", #call, hipGetErrorString(_e));               \
+            return -1;                                                                 \
+        }                                                                              \
+    } while (0)
+// propagate a nonzero status of an internal host helper
+#define ZK_TRY(expr)                \
+    do {                            \
+        const int _rc = (expr);     \
+        if (_rc != 0) return _rc;   \
+    } while (0)

@@ -86,6 +86,7 @@ __device__ uint64_t g_clprof[64][3][64];   // [wg][0: loader before wait, 1: loa
 __device__ uint64_t g_clprof_end[64][2];   // compute wave: after the MFMAs of the last step, at the end
 __device__ uint64_t g_clprof_rt[64][6];    // wave 0: realtime at start, first barrier, loop end, epilogue end; memtime at start, end
 __device__ uint64_t g_clwg[4096][2];       // every workgroup < 4096: realtime at start / end of wave 0
+__device__ uint32_t g_clhw[4096][8];       // every workgroup < 4096: HW_ID of waves 0-5, XCC_ID
 #define ZK_CL_STAMP(role, st)                                                                          \
     do {                                                                                               \
         if (blockIdx.x < 64 && (st) < 64 && lane == 0) g_clprof[blockIdx.x][role][st] = __builtin_amdgcn_s_memtime(); \
@@ -107,40 +108,56 @@ constexpr int CL_NW = CL_DA + 2;         // weight ring slots
 constexpr int CL_NLD = ZK_CL_NLD;        // loader waves (LDS-DMA issue is the per-step limit with one)
 constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 
-// Loader-wave implicit GEMM. Wave 4 only moves bytes (LDS-DMA) and counts its own vmcnt;
-// waves 0-3 only read LDS + MFMA, so the vmcnt(0) that hipcc places before their ds_reads
+// Loader-wave implicit GEMM, persistent. Waves 4.. only move bytes (LDS-DMA) and count their own
+// vmcnt; waves 0-3 only read LDS + MFMA, so the vmcnt(0) that hipcc places before their ds_reads
 // (it cannot tell the DMA's LDS range) costs nothing -- they have no loads in flight.
 // Step i = (chunk c, tap t); the loader runs CL_DA steps ahead for weights and DX steps
 // ahead for windows (DX >= CL_DA, window ring of NX slots), one raw s_barrier per step.
+// Persistent: the grid holds as many workgroups as are resident at once (2 per CU), and each walks
+// its share of the (row, position tile, channel tile) tiles as ONE step stream: the loaders run
+// into the next tile while the compute waves store this one, and no workgroup waits to be
+// dispatched (a one-tile-per-workgroup grid kept 58 % of the slots busy: the dispatcher waits for
+// a free slot on the XCD the next workgroup id is bound to).
 // DA: weight slices the loader keeps in flight (ring of DA + 2 slots); OCC: workgroups per CU the
 // registers are sized for
-template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2>
+// NWY: position waves (2 compute waves per position range: the two channel halves), NLDK loader
+// waves: 2 x NWY + NLDK waves per workgroup.
+template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2, int NWY = 2, int NLDK = CL_NLD>
 #ifndef ZK_CL_LBW
-#define ZK_CL_LBW(OCC_) ((OCC_ * CL_THREADS + 255) / 256)
+#define ZK_CL_LBW(OCC_, NT_) ((OCC_ * (NT_) + 255) / 256)
 #endif
-__global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
+__global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY + NLDK))) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
     int out_off0, int Tout, const float* resid, float* xout, const float* __restrict__ alpha,
     void* __restrict__ sout, int s_f32, const int32_t* __restrict__ lens, int in_scale, int out_scale, int nq,
-    int nx_slots, int dx) {
+    int nx_slots, int dx, int B) {
     constexpr int CI = 32;
     using I = Img<CI>;
     constexpr int CO_T = 32 * FM;
     constexpr int WS = CO_T * I::RB;             // weight slot bytes
     constexpr int NWP = CO_T / 16;               // weight pieces (1 KiB = 16 rows) per step
-    extern __shared__ __attribute__((aligned(16))) char smem[];   // [W ring][X ring], one array
+    constexpr int NCW = 2 * NWY;                 // compute waves
+    constexpr int QTT = 16 * NQ * NWY;           // positions per tile
+    extern __shared__ __attribute__((aligned(16))) char smem[];   // [W ring][X ring][epilogue tables x 2]
 
-    // XCD-aware decode of the 1-D grid: the workgroups an XCD receives (ids = xcd mod 8) walk
-    // co-tiles fastest, so one window is re-read from that XCD's L2 rather than from HBM.
+    // Tiles: XCD x (= blockIdx.x % 8 under round-robin dispatch) owns the contiguous range [lo, hi)
+    // of the tile order (channel tile fastest, then position tile, then row), and its
+    // gridDim.x / 8 workgroups stride through it, so the co-tiles of one window run side by side
+    // on one XCD and re-read the window from its L2 rather than from HBM.
     const int nco = (Cout / CO_T) * nphase;
-    const int nwg = gridDim.x, id = blockIdx.x;
-    const int xcd = id & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int L = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (id >> 3);
-    const int cot = L % nco, qtile = (L / nco) % nq, b = L / (nco * nq);
-    const int phase = cot % nphase, co0 = (cot / nphase) * CO_T;
-    constexpr int QTT = 32 * NQ;
-    const int q0 = qtile * QTT;
+    const int ntiles = B * nq * nco;
+    const int kx = blockIdx.x >> 3, nper = gridDim.x >> 3;
+    const int lo = (int)((long)(blockIdx.x & 7) * ntiles / 8), hi = (int)((long)((blockIdx.x & 7) + 1) * ntiles / 8);
+    const int nt = hi - lo > kx ? (hi - lo - kx + nper - 1) / nper : 0;
+    auto tile_of = [&](int i, int& b, int& phase, int& co0, int& q0) {
+        const int L = lo + kx + i * nper;
+        const int cot = L % nco;
+        b = L / (nco * nq);
+        q0 = ((L / nco) % nq) * QTT;
+        phase = cot % nphase;
+        co0 = (cot / nphase) * CO_T;
+    };
 
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int win = QTT + (ks - 1) * dil;
@@ -151,21 +168,23 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
     const int nchunk = Cin / CI, nstep = nchunk * ks;
 
 #ifdef ZK_CL_PROF
+    if (blockIdx.x < 4096 && lane == 0 && wv < 6) {
+        g_clhw[blockIdx.x][wv] = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_REG_HW_ID
+        if (wv == 0) g_clhw[blockIdx.x][6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+    }
     if (wv == 0 && blockIdx.x < 4096 && lane == 0) g_clwg[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
     if (wv == 0 && blockIdx.x < 64 && lane == 0) {
         g_clprof_rt[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
         g_clprof_rt[blockIdx.x][4] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    if (wv >= 4) {
-        // ---------------- loader waves: loader lw moves the pieces p with p % CL_NLD == lw
+    if (wv >= NCW) {
+        // ---------------- loader waves: loader lw moves the pieces p with p % NLDK == lw
         // wave-uniform (readfirstlane): the piece counts and the vmcnt switch below stay scalar;
         // derived from threadIdx they would be per-lane values and the 64-way wait_vm switch a
         // chain of exec-masked branches (the loader then paced every step: convs +20 %)
-        const int lw = __builtin_amdgcn_readfirstlane(wv - 4);
-        const int len_in = lens ? min(lens[b] * in_scale, Tin) : Tin;
+        const int lw = __builtin_amdgcn_readfirstlane(wv - NCW);
         const size_t wtap = (size_t)Cout * Cin;
-        const int u0 = q0 - pad;
         // A 1 KiB piece = 16 rows x 4 16-B slots; lane -> (row prow, slot pslot). With CI = 32 the
         // image swizzle of row p*16 + prow does not depend on the piece p, so this lane's source
         // offset inside any piece is one constant: no per-piece index math on the loader's path
@@ -176,29 +195,49 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
         const int g = pslot ^ I::swz(prow);
         const int loff = prow * Cin + g * 8;
         const long prs = 16L * Cin;                                  // elements per 16-row piece
-        const uint16_t* xsrc0 = in + (size_t)b * Tin * Cin + loff + (long)u0 * Cin;   // row u0 of the window
-        const uint16_t* wsrc0 = w + (size_t)phase * wphase + (size_t)co0 * Cin + loff;
-        // every window row inside [0, len_in): no per-lane range checks (rows past `win` are read but unused)
-        const bool xfast = u0 >= 0 && u0 + nxp * 16 <= len_in;
-        const int nxl = (nxp - lw + CL_NLD - 1) / CL_NLD, nwl = (NWP - lw + CL_NLD - 1) / CL_NLD;
+        const int nxl = (nxp - lw + NLDK - 1) / NLDK, nwl = (NWP - lw + NLDK - 1) / NLDK;
+        // window stream (global step sx = j + dx): tile ix, tap tx, chunk cx; the tile's source row u0
+        int ix = 0, tx = 0, cx = 0, u0 = 0, len_in = Tin;
+        bool xfast = false;
+        const uint16_t* xsrc0 = in;
+        auto set_xtile = [&](int i) {
+            int b_, ph_, co_, q_;
+            tile_of(i, b_, ph_, co_, q_);
+            len_in = lens ? min(lens[b_] * in_scale, Tin) : Tin;
+            u0 = q_ - pad;
+            xsrc0 = in + (size_t)b_ * Tin * Cin + loff + (long)u0 * Cin;     // row u0 of the window
+            // every window row inside [0, len_in): no per-lane range checks (rows past `win` are read but unused)
+            xfast = u0 >= 0 && u0 + nxp * 16 <= len_in;
+        };
+        // weight stream (global step sw = j + DA): tile iw, tap tw, chunk cw
+        int iw = 0, tw = 0, cw = 0;
+        const uint16_t* wsrc0 = w;
+        auto set_wtile = [&](int i) {
+            int b_, ph_, co_, q_;
+            tile_of(i, b_, ph_, co_, q_);
+            wsrc0 = w + (size_t)ph_ * wphase + (size_t)co_ * Cin + loff;
+        };
+        if (nt > 0) {
+            set_xtile(0);
+            set_wtile(0);
+        }
+        int xslot = 0, wslot = 0;                    // ring slots: one stream across the tiles
         int hist[DA + 1] = {};                       // loads issued by iterations j-DA .. j
-        int tx = 0, cx = 0, xslot = 0;               // window stream at sx = j + dx: tap, chunk, ring slot
-        int tw = 0, cw = 0, wslot = 0;               // weight stream at sw = j + DA (once sw >= 0)
-        for (int j = -dx; j < nstep; ++j) {
+        const int total = nt * nstep;
+        for (int j = -dx; j < total; ++j) {
             int nl = 0;
             // window first: a window issued in the same iteration as W(j+DA) is then older
             // than it, so waiting for W(j) below also covers every window step j can need
-            const int sx = j + dx;
-            if (sx < nstep) {
+            if (ix < nt) {
                 if (tx == 0) {
                     char* dst = xring + xslot * XS;
                     const uint16_t* src = xsrc0 + cx * CI;
                     if (xfast) {
-                        for (int p = lw; p < nxp; p += CL_NLD)
+                        for (int p = lw; p < nxp; p += NLDK)
                             __builtin_amdgcn_global_load_lds((const void*)(src + p * prs), (void*)(dst + p * 1024), 16,
                                                              0, 0);
                     } else {
-                        for (int p = lw; p < nxp; p += CL_NLD) {
+                        for (int p = lw; p < nxp; p += NLDK) {
                             const int row = p * 16 + prow, u = u0 + row;
                             const void* sp = (row < win && u >= 0 && u < len_in) ? (const void*)(src + p * prs)
                                                                                  : (const void*)g_zero_page;
@@ -208,16 +247,21 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
                     nl += nxl;
                     if (++xslot == nx_slots) xslot = 0;
                 }
-                if (++tx == ks) { tx = 0; ++cx; }
+                if (++tx == ks) {
+                    tx = 0;
+                    if (++cx == nchunk) {
+                        cx = 0;
+                        if (++ix < nt) set_xtile(ix);
+                    }
+                }
             }
-            const int sw = j + DA;
-            if (sw >= 0 && sw < nstep) {
-                if (!ZK_CL_DIAG_NOW || sw < DA + 2) {     // (diag: each weight slot filled once)
+            if (j + DA >= 0 && iw < nt) {
+                if (!ZK_CL_DIAG_NOW || j + DA < DA + 2) {     // (diag: each weight slot filled once)
                     char* dst = wring + wslot * WS;
                     const uint16_t* src = wsrc0 + tw * wtap + cw * CI;
 #pragma unroll
-                    for (int pp = 0; pp < (NWP + CL_NLD - 1) / CL_NLD; ++pp) {
-                        const int p = pp * CL_NLD + lw;
+                    for (int pp = 0; pp < (NWP + NLDK - 1) / NLDK; ++pp) {
+                        const int p = pp * NLDK + lw;
                         if (p >= NWP) break;
                         __builtin_amdgcn_global_load_lds((const void*)(src + p * prs), (void*)(dst + p * 1024), 16, 0,
                                                          0);
@@ -225,7 +269,13 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
                     nl += nwl;
                 }
                 if (++wslot == DA + 2) wslot = 0;
-                if (++tw == ks) { tw = 0; ++cw; }
+                if (++tw == ks) {
+                    tw = 0;
+                    if (++cw == nchunk) {
+                        cw = 0;
+                        if (++iw < nt) set_wtile(iw);
+                    }
+                }
             }
 #pragma unroll
             for (int k = 0; k < DA; ++k) hist[k] = hist[k + 1];
@@ -244,143 +294,152 @@ __global__ __launch_bounds__(CL_THREADS, ZK_CL_LBW(OCC)) void k_conv_cl(
         return;
     }
 
-    // ---------------- compute waves 0-3: 2 (co) x 2 (positions)
-    const int ln = lane & 15, lg = lane >> 4, wm = wv >> 1, wn = wv & 1;
-    f32x4 acc[FM][NQ];
-#pragma unroll
-    for (int m = 0; m < FM; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // Epilogue constants of this workgroup's CO_T channels -- bias, Snake alpha, 1/(alpha + 1e-9) --
-    // staged into an LDS table while the loader fills the rings (the epilogue used to start with
-    // their global loads and four IEEE divisions per channel quartet)
-    float* const ept = reinterpret_cast<float*>(xring + nx_slots * XS);
-    for (int i = tid; i < CO_T; i += 256) {
-        const float a_ = sout ? alpha[co0 + i] : 1.f;
-        ept[i] = bias[co0 + i];
-        ept[CO_T + i] = a_;
-        ept[2 * CO_T + i] = __fdiv_rn(1.0f, __fadd_rn(a_, 1e-9f));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // visible after the first barrier
-    const int len_out = lens ? lens[b] * out_scale : Tout;
-
-    // RES (resid != nullptr: the 1x1 convs of the residual units): the residual tile is loaded
-    // before the main loop, so its latency overlaps the loader's first DMA instead of following
-    // the last MFMA (clamped, unconditional loads; out-of-range positions are never stored).
-    // A separate instantiation: the 64 extra registers would cost the k7 convs occupancy.
-    float4 rv[RES ? FM : 1][NQ];
-    if constexpr (RES) {
+    // ---------------- compute waves 0 .. NCW-1: 2 (co) x NWY (positions)
+    const int ln = lane & 15, lg = lane >> 4, wm = wv / NWY, wn = wv % NWY;
+    int t = 0, xslot = 0, wslot = 0;             // tap, window ring slot, weight ring slot of the step
+    for (int it = 0; it < nt; ++it) {
+        int b, phase, co0, q0;
+        tile_of(it, b, phase, co0, q0);
+        f32x4 acc[FM][NQ];
 #pragma unroll
         for (int m = 0; m < FM; ++m)
+#pragma unroll
+            for (int n = 0; n < NQ; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        // Epilogue constants of this tile's CO_T channels -- bias, Snake alpha, 1/(alpha + 1e-9) --
+        // staged into an LDS table (two, by tile parity: a wave may still read the previous tile's)
+        // while the steps run (the epilogue used to start with their global loads and four IEEE
+        // divisions per channel quartet)
+        float* const ept = reinterpret_cast<float*>(xring + nx_slots * XS) + (it & 1) * 3 * CO_T;
+        for (int i = tid; i < CO_T; i += 64 * NCW) {
+            const float a_ = sout ? alpha[co0 + i] : 1.f;
+            ept[i] = bias[co0 + i];
+            ept[CO_T + i] = a_;
+            ept[2 * CO_T + i] = __fdiv_rn(1.0f, __fadd_rn(a_, 1e-9f));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // visible after the next barrier
+        const int len_out = lens ? lens[b] * out_scale : Tout;
+
+        // RES (resid != nullptr: the 1x1 convs of the residual units): the residual tile is loaded
+        // before the main loop, so its latency overlaps the steps instead of following the last
+        // MFMA (clamped, unconditional loads; out-of-range positions are never stored). A separate
+        // instantiation: the 64 extra registers would cost the k7 convs occupancy.
+        float4 rv[RES ? FM : 1][NQ];
+        if constexpr (RES) {
+#pragma unroll
+            for (int m = 0; m < FM; ++m)
+#pragma unroll
+                for (int n = 0; n < NQ; ++n) {
+                    const int q = q0 + wn * 16 * NQ + n * 16 + ln;
+                    const int tt = min(max(q * out_stride + out_off0 + phase, 0), Tout - 1);
+                    rv[m][n] = *reinterpret_cast<const float4*>(
+                        resid + ((size_t)b * Tout + tt) * Cout + co0 + wm * 16 * FM + m * 16 + lg * 4);
+                }
+        }
+
+        for (int s = 0; s < nstep; ++s) {
+            __builtin_amdgcn_s_barrier();            // step s is in LDS
+            asm volatile("" ::: "memory");
+            if (wv == 0 && it == 0) ZK_CL_STAMP(2, s);
+#ifdef ZK_CL_PROF
+            if (it == 0 && s == 0 && wv == 0 && blockIdx.x < 64 && lane == 0)
+                g_clprof_rt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
+            const char* xb = xring + xslot * XS;
+            const char* wb = wring + wslot * WS;
+            if (++wslot == DA + 2) wslot = 0;
+            uint4 a[FM], bq[NQ];
+#pragma unroll
+            for (int m = 0; m < FM; ++m)
+                a[m] = *reinterpret_cast<const uint4*>(wb + I::off(wm * 16 * FM + m * 16 + ln, lg));
+#pragma unroll
+            for (int n = 0; n < NQ; ++n)
+                bq[n] = *reinterpret_cast<const uint4*>(xb + I::off(wn * 16 * NQ + n * 16 + ln + t * dil, lg));
+            if (ZK_CL_DIAG_NOMFMA) {          // diag: keep the operand reads, drop the MFMAs
+#pragma unroll
+                for (int m = 0; m < FM; ++m)
+#pragma unroll
+                    for (int n = 0; n < NQ; ++n) acc[m][n][0] += __uint_as_float(a[m].x ^ bq[n].y);
+            } else {
+#pragma unroll
+                for (int m = 0; m < FM; ++m)
+#pragma unroll
+                    for (int n = 0; n < NQ; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a[m]), as_h8(bq[n]), acc[m][n], 0, 0,
+                                                                           0);
+            }
+            if (++t == ks) {
+                t = 0;
+                if (++xslot == nx_slots) xslot = 0;
+            }
+        }
+
+#ifdef ZK_CL_PROF
+        if (it == 0 && wv == 0 && blockIdx.x < 64 && lane == 0) {
+            float keep = 0.f;
+#pragma unroll
+            for (int m = 0; m < FM; ++m)
+#pragma unroll
+                for (int n = 0; n < NQ; ++n) keep += acc[m][n][0];
+            g_clprof_end[blockIdx.x][0] = __builtin_amdgcn_s_memtime() + (keep == 1.2345f);
+            g_clprof_rt[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
+        // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 16NQ wn + 16n + ln]
+        const int out_off = out_off0 + phase;
+#pragma unroll
+        for (int m = 0; m < FM; ++m) {
+            const int cl = wm * 16 * FM + m * 16 + lg * 4, co = co0 + cl;
+            const float4 bb = *reinterpret_cast<const float4*>(ept + cl);
+            const float4 aa = *reinterpret_cast<const float4*>(ept + CO_T + cl);
+            const float4 rr = *reinterpret_cast<const float4*>(ept + 2 * CO_T + cl);
+            const float r0 = rr.x, r1 = rr.y, r2 = rr.z, r3 = rr.w;
 #pragma unroll
             for (int n = 0; n < NQ; ++n) {
                 const int q = q0 + wn * 16 * NQ + n * 16 + ln;
-                const int tt = min(max(q * out_stride + out_off0 + phase, 0), Tout - 1);
-                rv[m][n] = *reinterpret_cast<const float4*>(
-                    resid + ((size_t)b * Tout + tt) * Cout + co0 + wm * 16 * FM + m * 16 + lg * 4);
-            }
-    }
-
-    int t = 0, xslot = 0, wslot = 0;             // tap, window ring slot, weight ring slot of step s
-    for (int s = 0; s < nstep; ++s) {
-        __builtin_amdgcn_s_barrier();            // step s is in LDS
-        asm volatile("" ::: "memory");
-        if (wv == 0) ZK_CL_STAMP(2, s);
-#ifdef ZK_CL_PROF
-        if (s == 0 && wv == 0 && blockIdx.x < 64 && lane == 0) g_clprof_rt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
-#endif
-        const char* xb = xring + xslot * XS;
-        const char* wb = wring + wslot * WS;
-        if (++wslot == DA + 2) wslot = 0;
-        uint4 a[FM], bq[NQ];
-#pragma unroll
-        for (int m = 0; m < FM; ++m)
-            a[m] = *reinterpret_cast<const uint4*>(wb + I::off(wm * 16 * FM + m * 16 + ln, lg));
-#pragma unroll
-        for (int n = 0; n < NQ; ++n)
-            bq[n] = *reinterpret_cast<const uint4*>(xb + I::off(wn * 16 * NQ + n * 16 + ln + t * dil, lg));
-        if (ZK_CL_DIAG_NOMFMA) {          // diag: keep the operand reads, drop the MFMAs
-#pragma unroll
-            for (int m = 0; m < FM; ++m)
-#pragma unroll
-                for (int n = 0; n < NQ; ++n) acc[m][n][0] += __uint_as_float(a[m].x ^ bq[n].y);
-        } else {
-#pragma unroll
-            for (int m = 0; m < FM; ++m)
-#pragma unroll
-                for (int n = 0; n < NQ; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(a[m]), as_h8(bq[n]), acc[m][n], 0, 0, 0);
-        }
-        if (++t == ks) {
-            t = 0;
-            if (++xslot == nx_slots) xslot = 0;
-        }
-    }
-
-#ifdef ZK_CL_PROF
-    if (wv == 0 && blockIdx.x < 64 && lane == 0) {
-        float keep = 0.f;
-#pragma unroll
-        for (int m = 0; m < FM; ++m)
-#pragma unroll
-            for (int n = 0; n < NQ; ++n) keep += acc[m][n][0];
-        g_clprof_end[blockIdx.x][0] = __builtin_amdgcn_s_memtime() + (keep == 1.2345f);
-        g_clprof_rt[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-    // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 16NQ wn + 16n + ln]
-    const int out_off = out_off0 + phase;
-#pragma unroll
-    for (int m = 0; m < FM; ++m) {
-        const int cl = wm * 16 * FM + m * 16 + lg * 4, co = co0 + cl;
-        const float4 bb = *reinterpret_cast<const float4*>(ept + cl);
-        const float4 aa = *reinterpret_cast<const float4*>(ept + CO_T + cl);
-        const float4 rr = *reinterpret_cast<const float4*>(ept + 2 * CO_T + cl);
-        const float r0 = rr.x, r1 = rr.y, r2 = rr.z, r3 = rr.w;
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) {
-            const int q = q0 + wn * 16 * NQ + n * 16 + ln;
-            const int tt = q * out_stride + out_off;
-            if (q >= Qn || tt < 0 || tt >= Tout) continue;
-            const size_t o = ((size_t)b * Tout + tt) * Cout + co;
-            float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-            if (tt < len_out) {
-                v0 = __fadd_rn(acc[m][n][0], bb.x);
-                v1 = __fadd_rn(acc[m][n][1], bb.y);
-                v2 = __fadd_rn(acc[m][n][2], bb.z);
-                v3 = __fadd_rn(acc[m][n][3], bb.w);
-                if constexpr (RES) {
-                    const float4 r = rv[m][n];
-                    v0 = __fadd_rn(r.x, v0);
-                    v1 = __fadd_rn(r.y, v1);
-                    v2 = __fadd_rn(r.z, v2);
-                    v3 = __fadd_rn(r.w, v3);
+                const int tt = q * out_stride + out_off;
+                if (q >= Qn || tt < 0 || tt >= Tout) continue;
+                const size_t o = ((size_t)b * Tout + tt) * Cout + co;
+                float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+                if (tt < len_out) {
+                    v0 = __fadd_rn(acc[m][n][0], bb.x);
+                    v1 = __fadd_rn(acc[m][n][1], bb.y);
+                    v2 = __fadd_rn(acc[m][n][2], bb.z);
+                    v3 = __fadd_rn(acc[m][n][3], bb.w);
+                    if constexpr (RES) {
+                        const float4 r = rv[m][n];
+                        v0 = __fadd_rn(r.x, v0);
+                        v1 = __fadd_rn(r.y, v1);
+                        v2 = __fadd_rn(r.z, v2);
+                        v3 = __fadd_rn(r.w, v3);
+                    }
                 }
+                if (xout) *reinterpret_cast<float4*>(xout + o) = make_float4(v0, v1, v2, v3);
+                if (!sout) continue;
+                // fp32 Snake output for the fp32 tail (exact sinf, reference formula); a separate
+                // instantiation so the common epilogue stays small enough to unroll fully (the
+                // accumulators then never leave registers)
+                if (SF32)
+                    reinterpret_cast<float4*>(sout)[o >> 2] =
+                        make_float4(snake(v0, aa.x), snake(v1, aa.y), snake(v2, aa.z), snake(v3, aa.w));
+                else
+                    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(sout) + o) =
+                        pack_h4(snake_fast(v0, aa.x, r0), snake_fast(v1, aa.y, r1), snake_fast(v2, aa.z, r2),
+                                snake_fast(v3, aa.w, r3));
             }
-            if (xout) *reinterpret_cast<float4*>(xout + o) = make_float4(v0, v1, v2, v3);
-            if (!sout) continue;
-            // fp32 Snake output for the fp32 tail (exact sinf, reference formula); a separate
-            // instantiation so the common epilogue stays small enough to unroll fully (the
-            // accumulators then never leave registers)
-            if (SF32)
-                reinterpret_cast<float4*>(sout)[o >> 2] =
-                    make_float4(snake(v0, aa.x), snake(v1, aa.y), snake(v2, aa.z), snake(v3, aa.w));
-            else
-                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(sout) + o) =
-                    pack_h4(snake_fast(v0, aa.x, r0), snake_fast(v1, aa.y, r1), snake_fast(v2, aa.z, r2),
-                            snake_fast(v3, aa.w, r3));
         }
+#ifdef ZK_CL_PROF
+        if (it == 0 && wv == 0 && blockIdx.x < 64 && lane == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            g_clprof_rt[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
+            g_clprof_rt[blockIdx.x][5] = __builtin_amdgcn_s_memtime();
+        }
+#endif
     }
 #ifdef ZK_CL_PROF
     if (wv == 0 && blockIdx.x < 4096 && lane == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         g_clwg[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (wv == 0 && blockIdx.x < 64 && lane == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        g_clprof_rt[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime();
-        g_clprof_rt[blockIdx.x][5] = __builtin_amdgcn_s_memtime();
     }
 #endif
 }
@@ -574,20 +633,37 @@ __global__ __launch_bounds__(256) void k_rvq_encode(const float* __restrict__ z,
     }
 }
 
-template <int FM, int NQ, int DA = CL_DA, int OCC = 2>
-void launch_conv(int nwg, size_t lds, hipStream_t st, const uint16_t* in, int Cin, int Tin, const uint16_t* w,
-                 long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn, int nphase,
-                 int out_stride, int out_off0, int Tout, const float* resid, float* xout, const float* alpha,
-                 void* sout, int s_f32, const int32_t* lens, int in_scale, int out_scale, int nq, int nx, int dx) {
-    auto kern = &k_conv_cl<FM, false, false, NQ, DA, OCC>;     // NQ = 8: fp16 output, no residual only
-    if constexpr (NQ == 4 && DA == CL_DA)
+// Persistent grid: as many workgroups as are resident at once (occupancy query for this kernel and
+// LDS size x CUs), a multiple of 8 (the kernel's XCD split), at most one per tile.
+template <int FM, int NQ, int NWY = 2, int NLDK = CL_NLD, int DA = CL_DA, int OCC = 2>
+int launch_conv(long ntiles, size_t lds, hipStream_t st, const uint16_t* in, int B, int Cin, int Tin,
+                const uint16_t* w, long wphase, const float* bias, int Cout, int ks, int dil, int pad, int Qn,
+                int nphase, int out_stride, int out_off0, int Tout, const float* resid, float* xout,
+                const float* alpha, void* sout, int s_f32, const int32_t* lens, int in_scale, int out_scale, int nq,
+                int nx, int dx) {
+    constexpr int NT = 64 * (2 * NWY + NLDK);
+    auto kern = &k_conv_cl<FM, false, false, NQ, DA, OCC, NWY, NLDK>;     // NQ = 8: fp16 output, no residual only
+    if constexpr (NQ == 4 && DA == CL_DA && NWY == 2)
         kern = resid ? (s_f32 ? &k_conv_cl<FM, true, true, NQ> : &k_conv_cl<FM, false, true, NQ>)
                      : (s_f32 ? &k_conv_cl<FM, true, false, NQ> : kern);
     if (lds > 65536)
-        hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(CL_THREADS), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0;
+        ZK_HIP(hipGetDevice(&dev));
+        ZK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    int occ = 0;
+    ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kern), NT, lds));
+    ZK_REQUIRE(occ >= 1, "zk_dac_conv_cl: kernel does not fit a CU (LDS %zu)", lds);
+    const long resident = (long)ncu * occ / 8 * 8;
+    const long grid = std::min<long>((ntiles + 7) / 8 * 8, std::max<long>(resident, 8));
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
                        dil, pad, Qn, nphase, out_stride, out_off0, Tout, resid, xout, alpha, sout, s_f32, lens,
-                       in_scale, out_scale, nq, nx, dx);
+                       in_scale, out_scale, nq, nx, dx, B);
+    return 0;
 }
 
 }  // namespace
@@ -647,15 +723,28 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     // residual tile would not fit the registers beside twice the accumulators), and so do the
     // polyphase ConvTranspose convs (+12-22 % with 256, profiles/r1_dac_wide_tiles_ab.txt)
     // (one workgroup per CU with a deeper weight ring measured slower: DESIGN.md §6)
-    const bool wide = resid == nullptr && !s_f32 && nphase == 1 && FM <= 3;
-    const int qt = wide ? 2 * QT : QT;
+#ifndef ZK_CL_WIDE
+#define ZK_CL_WIDE 1
+#endif
+    const bool wide = ZK_CL_WIDE && resid == nullptr && !s_f32 && nphase == 1 && FM <= 3;
+    // fat: the wide convs as ONE workgroup per CU of 8 compute waves (2 channel halves x 4 position
+    // quarters, 512-position tiles) + 4 loaders = 12 waves, exactly 3 per SIMD. Two 6-wave
+    // workgroups per CU (the same compute per step) were co-resident only where the wave placement
+    // happened to balance the SIMDs (3 waves per SIMD is the register limit at 150 VGPRs): 1.3 per CU
+    // on average (tools/dac_conv_stamps.py HW_ID census); one workgroup also shares each weight slice
+    // among twice the waves.
+#ifndef ZK_CL_FAT
+#define ZK_CL_FAT 1
+#endif
+    const bool fat = ZK_CL_FAT && wide;
+    const int qt = fat ? 4 * QT : (wide ? 2 * QT : QT);
     const int win = qt + (ks - 1) * dil;
     const size_t xs = (size_t)((win + 15) / 16) * 1024;
     const size_t ws = (size_t)32 * FM * 64;
     const int da = CL_DA;
-    const size_t lds_cap = 80 * 1024;
+    const size_t lds_cap = fat ? 160 * 1024 : 80 * 1024;
     // window lead DX >= da steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
-    const size_t ept = (size_t)3 * 32 * FM * sizeof(float);          // epilogue constants table
+    const size_t ept = (size_t)2 * 3 * 32 * FM * sizeof(float);      // epilogue constants tables (x 2)
     int dx = std::max(da, ks), nx = 1 + (dx + 1 + ks - 1) / ks;
     while (dx > da && (da + 2) * ws + nx * xs + ept > lds_cap) {
         --dx;
@@ -664,19 +753,24 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     const size_t lds = (da + 2) * ws + nx * xs + ept;
     ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_conv_cl: LDS %zu too large", lds);
     const int nq = (Qn + qt - 1) / qt;
-    const long nwg = (long)B * nq * (Cout / (32 * FM)) * nphase;
-    ZK_REQUIRE(nwg < (1L << 31), "zk_dac_conv_cl: grid too large");
+    const long ntiles = (long)B * nq * (Cout / (32 * FM)) * nphase;
+    ZK_REQUIRE(ntiles < (1L << 31), "zk_dac_conv_cl: too many tiles");
     hipStream_t st = (hipStream_t)stream;
 #define ZK_CL(F_, NQ_)                                                                                           \
-    launch_conv<F_, NQ_>((int)nwg, lds, st, in, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad, Qn, nphase, \
-                         out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32, lens, in_scale, out_scale, nq, \
-                         nx, dx)
+    ZK_TRY((launch_conv<F_, NQ_>(ntiles, lds, st, in, B, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, pad, Qn,  \
+                                 nphase, out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out, s_f32, lens,   \
+                                 in_scale, out_scale, nq, nx, dx)))
+#define ZK_CLF(F_)                                                                                                \
+    ZK_TRY((launch_conv<F_, 8, 4, 4, CL_DA, 1>(ntiles, lds, st, in, B, Cin, Tin, w, w_phase_stride, bias, Cout, ks, dil, \
+                                     pad, Qn, nphase, out_stride, out_off0, Tout, resid, x_out, alpha_next, s_out,    \
+                                     s_f32, lens, in_scale, out_scale, nq, nx, dx)))
     switch (FM) {
         case 4: ZK_CL(4, 4); break;
-        case 3: if (wide) ZK_CL(3, 8); else ZK_CL(3, 4); break;
-        case 2: if (wide) ZK_CL(2, 8); else ZK_CL(2, 4); break;
-        default: if (wide) ZK_CL(1, 8); else ZK_CL(1, 4); break;
+        case 3: if (fat) ZK_CLF(3); else if (wide) ZK_CL(3, 8); else ZK_CL(3, 4); break;
+        case 2: if (fat) ZK_CLF(2); else if (wide) ZK_CL(2, 8); else ZK_CL(2, 4); break;
+        default: if (fat) ZK_CLF(1); else if (wide) ZK_CL(1, 8); else ZK_CL(1, 4); break;
     }
+#undef ZK_CLF
 #undef ZK_CL
     ZK_CHECK_LAUNCH("zk_dac_conv_cl");
     return 0;
@@ -691,6 +785,9 @@ extern "C" int zk_cl_prof_read(void* dst, void* dst_end) {
 extern "C" int zk_cl_prof_read_wg(void* dst) {
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_clwg), sizeof(g_clwg)) == hipSuccess ? 0 : -1;
 }
+extern "C" int zk_cl_prof_read_hw(void* dst) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_clhw), sizeof(g_clhw)) == hipSuccess ? 0 : -1;
+}
 #endif
 
 extern "C" int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias, float* out,
@@ -700,7 +797,8 @@ extern "C" int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* 
     const size_t lds = ((size_t)((C * 7 + 3) & ~3) + (size_t)(TAIL_T + 6) * (C + 4)) * sizeof(float);
     ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_tail_cl: C=%d too large", C);
     if (lds > 65536)
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tail_cl), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tail_cl), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
     hipLaunchKernelGGL(k_tail_cl, dim3((T + TAIL_T - 1) / TAIL_T, B), dim3(TAIL_T), lds, (hipStream_t)stream, s, C, T, w,
                        bias, out, lens, scale);
     ZK_CHECK_LAUNCH("zk_dac_tail_cl");
