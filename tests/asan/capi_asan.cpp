@@ -53,6 +53,24 @@ STUB(zk_dac_conv_cl, const uint16_t*, int, int, int, const uint16_t*, long, cons
      int, int, int, const float*, float*, const float*, void*, int, const int32_t*, int, int, void*)
 STUB(zk_dac_tail_cl, const float*, int, int, int, const float*, const float*, float*, const int32_t*, int, void*)
 
+// ---- internal entries of zonos_amd/csrc/warm.h (C++ linkage): a warm-up variant records as the launch it
+// replaces, so the per-layer launch counts below are the same with and without the L2 warm-up
+#include "../../zonos_amd/csrc/warm.h"
+static int g_warm = 0;              // launches that carried a warm-up descriptor
+ZkWarm zk_gemm_warm_desc(const void* W, int, int N, int K, int nsplit, int chunks) {
+    return ZkWarm{W, K, N / 64, nsplit, chunks};
+}
+int zk_resid_ln_warm(const float*, int, const void*, const void*, const void*, float, int, int, void*, void*, int,
+                     const int32_t*, ZkWarm warm, void*) {
+    g_warm += warm.W != nullptr;
+    return stub("zk_resid_ln");
+}
+int zk_gemm_bf16_warm(const void*, long, const void*, int, int, int, int, int, float*, void*, const int32_t*,
+                      ZkWarm warm, void*) {
+    g_warm += warm.W != nullptr;
+    return stub("zk_gemm_bf16");
+}
+
 static int g_bad = 0;
 #define CHECK(cond, ...)                                     \
     do {                                                     \
@@ -90,7 +108,10 @@ static void transformer(int n_layer, int small, int merge) {
     d.part = d.attn_work = (float*)P(0);
     d.st.scal = scal; d.st.K = 9; d.st.V = 1026; d.st.Ld = 2599; d.st.B = d.B;
     g_calls.clear();
+    g_warm = 0;
     CHECK(zk_decode_step(&d, nullptr) == 0, "zk_decode_step: %s", zk_last_error());
+    // full step: both k_resid_ln and the fc1 GEMM of every layer warm the next GEMM's weights
+    if (!small) CHECK(g_warm == 3 * n_layer, "L2 warm-up descriptors: %d", g_warm);
     // embed + per layer (small: 5 with merge, 5 without; else 7) + heads + 2 samples + eos
     const size_t per = small ? 5 : 7;
     CHECK(g_calls.size() == 1 + per * n_layer + 4, "decode step: %zu calls", g_calls.size());
@@ -99,7 +120,9 @@ static void transformer(int n_layer, int small, int merge) {
     if (small && merge) CHECK(count("zk_gemv_attn_out") == (size_t)n_layer, "merged out_proj per layer");
     // prefill
     g_calls.clear();
+    g_warm = 0;
     CHECK(zk_prefill(&d, P(0), 0, 10, P(0), nullptr) == 0, "zk_prefill: %s", zk_last_error());
+    CHECK(g_warm == 0, "prefill must not warm (%d)", g_warm);
     CHECK(g_calls.size() == 2 + 8 * (size_t)n_layer + 3, "prefill: %zu calls", g_calls.size());
     // error propagation: the 5th enqueue fails -> the step stops there and reports it
     g_calls.clear();
