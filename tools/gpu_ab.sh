@@ -10,6 +10,8 @@
 #   micro:MODE            tools/microbench.py MODE on the product library and every
 #                         zonos_amd/lib/variants/<v> (built on the CPU with
 #                         zonos_amd.build.build_variant), twice, interleaved
+#   benchv:NAME[:ARGS]    bench.py ARGS on the product library and every variant, twice,
+#                         interleaved -> OUT/benchv_NAME.log (value + decode ms per step)
 #   prof:NAME[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> OUT/prof_NAME/*stats.csv
 #   pmc:NAME:COUNTERS[:ARGS]  one rocprofv3 --pmc pass (COUNTERS comma-separated, within one
 #                         block's limits) of bench.py ARGS -> OUT/pmc_NAME/
@@ -38,6 +40,17 @@ for step in "$@"; do
         done
       done > "$OUT/micro_$rest.log" 2>&1
       grep -v amdgpu "$OUT/micro_$rest.log" ;;
+    benchv)
+      name=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      for i in 1 2; do
+        for v in product $(ls zonos_amd/lib/variants 2>/dev/null); do
+          lp=""; [ "$v" != product ] && lp=zonos_amd/lib/variants/$v/libzonos_hip.so
+          ZK_LIB_PATH=$lp timeout -k 10 400 python -u bench.py ${a//,/ } --no-cpu-baseline > "$OUT/benchv_tmp.log" 2>&1
+          grep '^{' "$OUT/benchv_tmp.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); b=d['breakdown']; print('$v', d['value'], b.get('decode_ms_per_token_step'), b.get('dac_s_per_step'))"
+        done
+      done > "$OUT/benchv_$name.log" 2>&1
+      rm -f "$OUT/benchv_tmp.log"
+      cat "$OUT/benchv_$name.log" ;;
     prof)
       name=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
