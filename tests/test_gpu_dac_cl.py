@@ -42,6 +42,7 @@ CONV_CASES = [  # Cin, Cout, ks, dil, T, resid
     (192, 192, 7, 3, 260, False),
     (1024, 1536, 7, 1, 40, False),
     (384, 384, 1, 1, 129, True),
+    (192, 192, 1, 1, 300, True),
 ]
 
 

@@ -1072,12 +1072,16 @@ extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int 
 #ifndef ZK_GF_PF2
 #define ZK_GF_PF2 ZK_GF_PF         // k-steps in flight of the B = 1 (XR = 2) instantiations
 #endif
+#ifndef ZK_GF_PFLN
+#define ZK_GF_PFLN 12              // k-steps in flight of the B = 1 LayerNorm-prologue one-tile GEMV (in_proj):
+#endif                             // c2 step 1.045-1.048 vs 1.051-1.053 ms at 8, 1.054-1.055 at 16 (r3_b1_gemv_pf_ab)
 #define ZK_GF(MODE_, LN_, NTW_, HALF_, NW_, KSW_)                                                            \
     do {                                                                                                      \
         constexpr int KS_ = (KSW_) / (NW_);                                                                   \
         constexpr int NL_ = HALF_ ? KS_ / 2 : KS_;                                                            \
+        constexpr int PB_ = (LN_ && NTW_ == 1 && !HALF_) ? ZK_GF_PFLN : ZK_GF_PF2;                            \
         if (M <= 2)                                                                               \
-            hipLaunchKernelGGL((k_gemv_f<MODE_, LN_, NTW_, HALF_, NW_, KS_, (NL_ < ZK_GF_PF2 ? NL_ : ZK_GF_PF2),  \
+            hipLaunchKernelGGL((k_gemv_f<MODE_, LN_, NTW_, HALF_, NW_, KS_, (NL_ < PB_ ? NL_ : PB_),              \
                                           0, 2>),                                                             \
                                dim3(grid), dim3(64 * (NW_)), 0, (hipStream_t)stream, (const bf16_t*)A, lda,    \
                                (const bf16_t*)W, M, N, K, (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, Cf,    \
