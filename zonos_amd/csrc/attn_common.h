@@ -83,29 +83,6 @@ ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int
     for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld_kv<NT>(v0 + dt * 512);
 }
 
-// LDS-DMA form of the same loads: the 8 x 1 KB pieces of one 32-key K (or V^T) slice go to 8
-// consecutive 1 KB ring slots, lane L's 16 B at byte 16 L (global_load_lds_dwordx4 is
-// lane-linear), so reading slot i at lane * 16 returns exactly what ld_kv would have loaded.
-// NT: the non-temporal cache policy (aux bit 1), as in ld_kv.
-template <bool NT>
-ZK_DEV void dma_kv(char* slots, const bf16_t* base, int key_base, int lane) {
-    const bf16_t* p = base + (size_t)(key_base >> 5) * 4096 + lane * 8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(p + i * 512), (void*)(slots + i * 1024), 16, 0, NT ? 2 : 0);
-}
-ZK_DEV void read_ring(uint4* dst, const char* slots, int lane) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dst[i] = *reinterpret_cast<const uint4*>(slots + i * 1024 + lane * 16);
-}
-template <int N_>
-ZK_DEV void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
-
-#ifndef ZK_ATT_DMA
-#define ZK_ATT_DMA 0       // LDS-DMA key loop for the large-cache (nt) regime
-#endif
-constexpr int AT_RING = 4 * 16 * 1024;   // LDS ring bytes per workgroup (4 waves x 16 slots x 1 KB)
-
 struct AttnState {
     float m, l;
     f32x4 o[8];      // o[dt][i] = O^T[d = dt*16 + 4lg + i][head = ln]
@@ -262,11 +239,11 @@ struct __attribute__((aligned(16))) AttnSmem {
 // kernel, whose loader wave must not take part); `issued` runs right after the first key blocks'
 // loads are in flight and before anything reads the in_proj output (the persistent kernel waits
 // for its in_proj seam there).
-template <bool FUSED, bool NEOX, bool KVNT, bool COMB, bool DMA, class Bar, class Issued>
-ZK_DEV void attn_decode_wg(AttnSmem& sm, char* ring_all, const Bar& bar, const Issued& issued, int split, int nsplit,
-                           int g, int r, const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H, int Hkv, int Smax,
-                           int ctx, float* work, float scale, bf16_t* out, const float* part, int gsplit,
-                           const float* freqs, uint32_t* cnt) {
+template <bool FUSED, bool NEOX, bool KVNT, bool COMB, class Bar, class Issued>
+ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, int split, int nsplit, int g, int r,
+                           const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H, int Hkv, int Smax, int ctx,
+                           float* work, float scale, bf16_t* out, const float* part, int gsplit, const float* freqs,
+                           uint32_t* cnt) {
     constexpr int HD = 128;
     auto& s_m = sm.s_m;
     auto& s_l = sm.s_l;
@@ -283,7 +260,6 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, char* ring_all, const Bar& bar, const I
     const int ln = lane & 15, lg = lane >> 4;
     bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
     bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
-    char* ring = ring_all + w * 16 * 1024;      // DMA: this wave's 16 slots
 
     bf16x8 qf[4];
     KVFrag fa, fb;
@@ -305,10 +281,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, char* ring_all, const Bar& bar, const I
     // that of reading the cache. The first key block can therefore be fetched before the prologue.
     const int pos = ctx - 1;
     const bool early = FUSED && kbw > kb0;
-    if (DMA && early) {      // the first key slice (16 KB) lands in the ring during the prologue
-        dma_kv<KVNT>(ring, kb, kb0 * AT_KB + 32 * w, lane);
-        dma_kv<KVNT>(ring + 8 * 1024, vb, kb0 * AT_KB + 32 * w, lane);
-    } else if (early) {      // the first TWO key blocks are in flight during the prologue
+    if (early) {      // the first TWO key blocks are in flight during the prologue
         load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         if (!ZK_ATT_TRIM || kb0 + 1 < kbw) load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
     }
@@ -381,38 +354,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, char* ring_all, const Bar& bar, const I
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (DMA) {
-        // LDS-DMA key loop: the wave's 32-key K and V^T slices (16 x 1 KB pieces) land in its own
-        // 16-slot LDS ring (slots 0-7 K, 8-15 V); the next slice's K pieces are issued as soon as
-        // this slice's K fragments are in registers, its V pieces after the V fragments: 8-16 KB
-        // in flight per wave with no VGPRs held for loads in flight.
-        if (kbw > kb0) {
-            if (!early) {
-                dma_kv<KVNT>(ring, kb, kb0 * AT_KB + 32 * w, lane);
-                dma_kv<KVNT>(ring + 8 * 1024, vb, kb0 * AT_KB + 32 * w, lane);
-            }
-            KVFrag& f = fa;
-            for (int it = kb0; it < kbw; ++it) {
-                const bool more = it + 1 < kbw;
-                vm_wait_n<8>();                                     // K(it) landed (V(it) may be in flight)
-                read_ring(f.k[0], ring, lane);
-                read_ring(f.k[1], ring + 4 * 1024, lane);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots free before they are refilled
-                if (more) {
-                    dma_kv<KVNT>(ring, kb, (it + 1) * AT_KB + 32 * w, lane);
-                    vm_wait_n<8>();                                 // V(it) landed, K(it+1) in flight
-                } else {
-                    vm_wait_n<0>();
-                }
-                read_ring(&f.v[0], ring + 8 * 1024, lane);
-                read_ring(&f.v[4], ring + 12 * 1024, lane);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (more) dma_kv<KVNT>(ring + 8 * 1024, vb, (it + 1) * AT_KB + 32 * w, lane);
-                if (FUSED) patch_kv(f, s_kn, s_vn, it * AT_KB + 32 * w, pos, ln, lg);
-                attn_step(st, f, qf, it * AT_KB + 32 * w, ctx, scale, lg);
-            }
-        }
-    } else if (kbw > kb0) {
+    if (kbw > kb0) {
         if (!early) load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         for (int it = kb0; it < kbw; it += 2) {
             if (!(early && it == kb0) && (!ZK_ATT_TRIM || it + 1 < kbw))
@@ -522,14 +464,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
                                                         float* work, float scale, bf16_t* out, const int32_t* skip,
                                                         const float* part, int gsplit, const float* freqs,
                                                         uint32_t* cnt = nullptr) {
-    constexpr bool DMA = ZK_ATT_DMA && KVNT;
     __shared__ AttnSmem sm;
-    __shared__ __attribute__((aligned(1024))) char ring[DMA ? AT_RING : 16];
     if (skip && *skip) return;
     const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
-    attn_decode_wg<FUSED, NEOX, KVNT, COMB, DMA>(sm, ring, [] { __syncthreads(); }, [] {}, blockIdx.x, gridDim.x,
-                                                blockIdx.y, blockIdx.z, q, kc, vt, R, H, Hkv, Smax, ctx, work, scale,
-                                                out, part, gsplit, freqs, cnt);
+    attn_decode_wg<FUSED, NEOX, KVNT, COMB>(sm, [] { __syncthreads(); }, [] {}, blockIdx.x, gridDim.x, blockIdx.y,
+                                           blockIdx.z, q, kc, vt, R, H, Hkv, Smax, ctx, work, scale, out, part,
+                                           gsplit, freqs, cnt);
 }
 
 }  // namespace
