@@ -43,8 +43,10 @@ GREEDY_SP = dict(temperature=0.0, top_p=0, top_k=0, min_p=0, linear=0.0, conf=0.
 FULL_CASES = {
     "c1": dict(B=1, Lc=24, P=0, T=129, emb_gain=4.0, logit_steps=(0, 1, 64, 128)),
     "c2": dict(B=1, Lc=160, P=0, T=861, windows=((0, 32), (800, 8)), utts=(0,), logit_steps=(0, 1, 31, 800, 807)),
-    "c3": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 8), (1290, 8)), utts=(0, 37),
-               logit_steps=(0, 1, 1290, 1291)),
+    # c3: five utterances spread over the batch (first, last, three inside) at the first steps, the
+    # mean context and the end of the 30 s workload (ctx up to Lc + P + 1 + 2567 = 2978)
+    "c3": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 8), (1290, 8), (2560, 8)), utts=(0, 13, 37, 50, 63),
+               logit_steps=(0, 1, 1290, 1291, 2560, 2567)),
     # c4 = B=512 over 8 GPUs: the rank-7 shard (utterances 448..511 -> row_base 448, the inputs
     # bench.py gives rank 7: conditioning seed 1+7, prefix seed 3+7), two utterances, at the first
     # steps and at the last steps of the 30 s workload (context up to Lc + P + 1 + 2587 = 2998)

@@ -8,7 +8,8 @@ heads 9x1026) of the HIP engine against golden vectors the REFERENCE produced
   benchmark's distribution), CLI sampling, EOS never accepted (benchmark mode). The engine runs
   the whole batch teacher-forced on a seeded synthetic history; its fp32 CFG logits and sampled
   tokens are compared with the reference's at the first steps and at a late context (c2: steps
-  0-31 and 800-807, ctx 961-968; c3: steps 0-7 and 1290-1297, ctx 1701-1708, utterances 0 and 37).
+  0-31 and 800-807, ctx 961-968; c3: steps 0-7, 1290-1297 and 2560-2567, ctx up to 2978, utterances
+  0, 13, 37, 50 and 63).
 * c4 -- B=512 over 8 GPUs: one rank's shard run as that rank runs it (the rank-7 shard: B=64,
   row_base 448 keys the sampling noise, rank 7's conditioning / prefix seeds), utterances 448 and
   485 at steps 0-3 and at the last steps 2584-2587 (ctx 2995-2998, the longest context).
