@@ -48,9 +48,9 @@ FULL_CASES = {
     "c3": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 8), (1290, 8), (2560, 8)), utts=(0, 13, 37, 50, 63),
                logit_steps=(0, 1, 1290, 1291, 2560, 2567)),
     # c4 = B=512 over 8 GPUs: the rank-7 shard (utterances 448..511 -> row_base 448, the inputs
-    # bench.py gives rank 7: conditioning seed 1+7, prefix seed 3+7), two utterances, at the first
+    # bench.py gives rank 7: conditioning seed 1+7, prefix seed 3+7), five utterances, at the first
     # steps and at the last steps of the 30 s workload (context up to Lc + P + 1 + 2587 = 2998)
-    "c4": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 4), (2584, 4)), utts=(0, 37), row_base=448,
+    "c4": dict(B=64, Lc=400, P=10, T=2580, windows=((0, 4), (2584, 4)), utts=(0, 13, 37, 50, 63), row_base=448,
                cond_seed=8, prefix_seed=10, hist_seed=14, hist_T=2590, logit_steps=(0, 1, 2584, 2587)),
 }
 FULL_SEED = 1234

@@ -11,8 +11,8 @@ heads 9x1026) of the HIP engine against golden vectors the REFERENCE produced
   0-31 and 800-807, ctx 961-968; c3: steps 0-7, 1290-1297 and 2560-2567, ctx up to 2978, utterances
   0, 13, 37, 50 and 63).
 * c4 -- B=512 over 8 GPUs: one rank's shard run as that rank runs it (the rank-7 shard: B=64,
-  row_base 448 keys the sampling noise, rank 7's conditioning / prefix seeds), utterances 448 and
-  485 at steps 0-3 and at the last steps 2584-2587 (ctx 2995-2998, the longest context).
+  row_base 448 keys the sampling noise, rank 7's conditioning / prefix seeds), utterances 448, 461,
+  485, 498 and 511 at steps 0-3 and at the last steps 2584-2587 (ctx 2995-2998, the longest context).
 """
 import numpy as np
 import pytest
