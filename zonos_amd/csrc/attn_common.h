@@ -235,10 +235,9 @@ struct __attribute__((aligned(16))) AttnSmem {
 };
 
 // One workgroup of 4 waves (threads 0..255) = one (split, kv head g, row r). `bar` is the barrier
-// among those 4 waves (__syncthreads in k_attn_decode; an LDS barrier inside the persistent step
-// kernel, whose loader wave must not take part); `issued` runs right after the first key blocks'
-// loads are in flight and before anything reads the in_proj output (the persistent kernel waits
-// for its in_proj seam there).
+// among those 4 waves (__syncthreads in k_attn_decode); `issued` runs right after the first key
+// blocks' loads are in flight and before anything reads the in_proj output or writes anything:
+// it returns true when the launch is to be skipped (generation finished).
 template <bool FUSED, bool NEOX, bool KVNT, bool COMB, class Bar, class Issued>
 ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, int split, int nsplit, int g, int r,
                            const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H, int Hkv, int Smax, int ctx,
@@ -285,7 +284,17 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
         load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         if (!ZK_ATT_TRIM || kb0 + 1 < kbw) load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
     }
-    issued();
+    if (issued()) {          // skip: nothing is written (the loads above are in bounds)
+        if (early) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) { keep_live(fa.k[h][ks]); keep_live(fb.k[h][ks]); }
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) { keep_live(fa.v[dt]); keep_live(fb.v[dt]); }
+        }
+        return;
+    }
     ZK_ATT_STAMP(1);
     if constexpr (FUSED) {
         // pairs: [0, G*64) q of heads g*G.., then 64 k pairs, then 64 v pairs
@@ -465,11 +474,15 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
                                                         const float* part, int gsplit, const float* freqs,
                                                         uint32_t* cnt = nullptr) {
     __shared__ AttnSmem sm;
-    if (skip && *skip) return;
-    const int ctx = ctx0 + (ctx_dev ? *ctx_dev : 0);
-    attn_decode_wg<FUSED, NEOX, KVNT, COMB>(sm, [] { __syncthreads(); }, [] {}, blockIdx.x, gridDim.x, blockIdx.y,
-                                           blockIdx.z, q, kc, vt, R, H, Hkv, Smax, ctx, work, scale, out, part,
-                                           gsplit, freqs, cnt);
+    // both step scalars in one round trip; the skip word is tested once the first key blocks'
+    // loads are in flight (issued -> return), so its latency overlaps theirs
+    const int sk = ld_word(skip);
+    // (clamped to the cache: a skipped launch after the last step may see ctx = Smax + 1, and its
+    // first key blocks are loaded before the skip test; every real step has ctx <= Smax)
+    const int ctx = min(ctx0 + uni(ld_word(ctx_dev)), Smax);
+    attn_decode_wg<FUSED, NEOX, KVNT, COMB>(sm, [] { __syncthreads(); }, [sk] { return uni(sk) != 0; }, blockIdx.x,
+                                           gridDim.x, blockIdx.y, blockIdx.z, q, kc, vt, R, H, Hkv, Smax, ctx, work,
+                                           scale, out, part, gsplit, freqs, cnt);
 }
 
 }  // namespace

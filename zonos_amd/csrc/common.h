@@ -9,6 +9,24 @@
 typedef uint16_t bf16_t;   // raw bf16 bits (torch.bfloat16 storage)
 typedef uint16_t f16_t;
 
+// ---------------------------------------------------------------- device step words
+// A nullable device int32 (skip / context / offset words) read without a branch and as a VECTOR
+// load (relaxed atomic: never scalarised), issued before the kernel's data loads: vmcnt retires in
+// issue order, so the test of the word waits for it alone, where a scalar load's wait (lgkmcnt(0),
+// scalar loads return out of order) would also hold every later kernel-argument load. Each lane
+// holds the same value; callers take it with readfirstlane where they branch or index on it.
+static __device__ int32_t zk_zero_word = 0;    // never written; not const, so the load is not folded
+ZK_DEV int32_t ld_word(const int32_t* p) {
+    return __hip_atomic_load(p != nullptr ? p : &zk_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+ZK_DEV int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// Use of loaded registers on a kernel's early-exit path: without a use there, hipcc sinks the
+// loads into the path that consumes them, i.e. below the exit test, which then waits for the
+// step word before the first data load is issued.
+ZK_DEV void keep_live(const uint4& v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
+ZK_DEV void keep_live(const uint2& v) { asm volatile("" ::"v"(v.x), "v"(v.y)); }
+ZK_DEV void keep_live(const float4& v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
+
 // ---------------------------------------------------------------- bf16 <-> f32
 // Round-to-nearest-even exactly like torch's float->bfloat16 conversion (c10/util/BFloat16.h),
 // NaN kept as a quiet NaN.

@@ -273,6 +273,8 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
                                                            const bf16_t* __restrict__ wW, int wK, int wgx, int wgz,
                                                            int wch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    // (the skip word is tested first here: deferring the test behind the first loads, as k_gemv_f
+    // does, measured 0.3-0.4 us slower per launch at c3, profiles/r3s2_skip_defer_ab.txt)
     if (skip && *skip) return;
     int bx, bz;
     ws_tile(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x, gridDim.z, bx, bz);     // gridDim.y == 1
@@ -510,7 +512,7 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
                                                     float* __restrict__ Cpart, bf16_t* __restrict__ Cout,
                                                     const int32_t* skip) {
     __shared__ __attribute__((aligned(16))) f32x4 red[4][NTW][64];
-    if (skip && *skip) return;
+    const int sk = ld_word(skip);                           // tested once the prefetch is in flight
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int split = blockIdx.z;
@@ -536,6 +538,16 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
     for (int p = 0; p < PF; ++p)
         if (p < KS) issue(p, p);
     __builtin_amdgcn_sched_barrier(0);
+    if (uni(sk)) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p)
+            if (p < KS) {
+                keep_live(ar[p]);
+#pragma unroll
+                for (int t = 0; t < NTW; ++t) keep_live(wr[p][t]);
+            }
+        return;
+    }
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
         if (st + PF < KS) issue(st + PF, (st + PF) % U);
@@ -643,7 +655,7 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     static_assert(!MRG || XR == 2, "merge prologue: M <= 2");
     __shared__ __attribute__((aligned(16))) uint4 xs[XS ? XR * GF_XS / 8 : 1];
     __shared__ __attribute__((aligned(16))) f32x4 red[NW][NTW][64];
-    if (skip && *skip) return;
+    const int sk = ld_word(skip);              // tested once the weight prefetch is in flight
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int nt0 = HALF ? (blockIdx.x >> 1) : blockIdx.x * NTW;    // first 16-column tile
@@ -725,6 +737,34 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
         if (p < NL) issue(p, p);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    if (uni(sk)) {                                      // every load above is in bounds; nothing written yet
+        // (the prologue / epilogue loads too: sunk below this test they would queue behind the
+        // weight prefetch and drain it when waited for)
+#pragma unroll
+        for (int p = 0; p < PF; ++p)
+            if (p < NL) {
+#pragma unroll
+                for (int tt = 0; tt < NTW; ++tt) keep_live(wr[p][tt]);
+            }
+        if constexpr (LN) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                keep_live(wv[j]);
+                keep_live(bv[j]);
+#pragma unroll
+                for (int rr = 0; rr < MR; ++rr) keep_live(xv[rr][j]);
+            }
+        }
+        if constexpr (MRG) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int sp = 0; sp < NS; ++sp)
+                    asm volatile("" ::"v"(mm[i][sp]), "v"(ml[i][sp]), "v"(mo[i][sp].x), "v"(mo[i][sp].y));
+        }
+        if constexpr (MODE == 2) asm volatile("" ::"v"((int)rv[0]), "v"((int)rv[1]), "v"((int)rv[2]), "v"((int)rv[3]));
+        return;
+    }
 
     if constexpr (LN) {
         // the row values pass through an empty asm here, so no arithmetic on them (and therefore

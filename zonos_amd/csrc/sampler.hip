@@ -298,12 +298,18 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
     const int B = st.B, K = st.K, V = st.V;
     const int b = blockIdx.x / K, k = blockIdx.x % K;
     const int32_t* scal = st.scal;
-    if (scal[3]) return;                                    // generation finished
+    // Every load that does not depend on another one is issued up front (one memory round trip):
+    // the done word, the step scalars, this row's state and the logits; the finished check comes
+    // after them (the loads are in bounds either way).
+    const int done = scal[3];
+    const int offset = scal[0], step = scal[2];
+    const float rpb = st.rp[b];
+    const int actb = st.act[b];
     int new_eos_b = 0;
     if (draw == 1) {   // EOS resample happens only if some row has a new EOS (model.py:380)
-        int any = 0;   // one row per thread: a single memory round trip
+        int any = 0;   // one row per thread
         for (int r = threadIdx.x; r < B; r += NT) any |= (st.tok0[r * K] == EOS) && !st.eos_mode[r];
-        if (!__syncthreads_or(any)) return;
+        if (!__syncthreads_or(any && !done)) return;
         new_eos_b = (st.tok0[b * K] == EOS) && !st.eos_mode[b];
     }
     const size_t N = (size_t)K * V;
@@ -311,8 +317,29 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
     const float* pc = part + (size_t)b * N + (size_t)k * V;
     const float* pu = part + (size_t)(b + B) * N + (size_t)k * V;
     float x[NPT];
+    if (nsplit == 1) {     // the unsplit heads GEMM (c3, B <= 8): all 2 x NPT loads before the first use
+        float c1[NPT], u1[NPT];
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int v = min(threadIdx.x + NT * i, V - 1);
+            c1[i] = pc[v];
+            u1[i] = pu[v];
+        }
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int v = threadIdx.x + NT * i;
+            float val = -INFINITY;
+            if (v < V) {
+                const float c = round_bf(0.f + c1[i]), u = round_bf(0.f + u1[i]);   // head output bf16 (model.py:111)
+                val = __fadd_rn(u, __fmul_rn(__fsub_rn(c, u), sp.cfg_scale));       // model.py:114
+                if (v >= 1025) val = -INFINITY;                                    // model.py:115
+            }
+            x[i] = val;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
+        if (nsplit == 1) break;
         const int v = threadIdx.x + NT * i;
         float val = -INFINITY;
         if (v < V) {
@@ -324,6 +351,7 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
         }
         x[i] = val;
     }
+    if (done) return;                                       // generation finished
     if (dbg != nullptr && draw == 0) {
         float* d = dbg + ((size_t)b * K + k) * V;
 #pragma unroll
@@ -337,15 +365,14 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
             if (!prefill) {
                 if (k >= 1) x[i] = -INFINITY;                                  // model.py:323
                 else x[i] = __fadd_rn(x[i], 0.0f - LOG1024F);                  // model.py:324,353
-                if (k == 0 && st.act[b]) x[i] = -INFINITY;                     // model.py:360-361
+                if (k == 0 && actb) x[i] = -INFINITY;                          // model.py:360-361
                 if (k == 0 && new_eos_b) x[i] = -INFINITY;                     // model.py:387
             }
             if (k == 0 && sp.force_full_length) x[i] = -INFINITY;              // benchmark mode
         }
     }
-    const int offset = scal[0];
     RowCtx c{b, k, V, prefill ? nullptr : st.delayed + ((size_t)b * K + k) * st.Ld, offset,
-             prefill ? 1.f : st.rp[b], prefill ? 0 : scal[2], draw, st.row_base + b, st.seed};
+             prefill ? 1.f : rpb, prefill ? 0 : step, draw, st.row_base + b, st.seed};
     const int t = sample_row(x, c, sp, s);
     if (threadIdx.x == 0) (draw ? st.tok1 : st.tok0)[b * K + k] = t;
 }
