@@ -475,43 +475,74 @@ __global__ __launch_bounds__(256) void k_rvq_cl(const int64_t* __restrict__ code
 // tile would be 1/16 used). fp32 here keeps the waveform within the fp32 reference's 1e-4.
 // The TAIL_T + 6 input rows of a workgroup are one contiguous [rows][C] block: staged into LDS
 // by whole float4 loads (row stride C + 4 floats: the 16 lanes of a ds_read_b128 hit distinct
-// banks), then each thread sums its position's 7 x C products in the order k, c.
-constexpr int TAIL_T = 128;
+// banks), then each thread sums its position's 7 x C products in the order k, c, in four chains
+// (c mod 4) added at the end.
+#ifndef ZK_TAIL_T
+#define ZK_TAIL_T 128
+#endif
+#ifndef ZK_TAIL_NB
+#define ZK_TAIL_NB 16
+#endif
+constexpr int TAIL_T = ZK_TAIL_T;    // positions (threads) per workgroup
 __global__ __launch_bounds__(TAIL_T) void k_tail_cl(const float* __restrict__ s, int C, int T,
                                                     const float* __restrict__ w, const float* __restrict__ bias,
                                                     float* __restrict__ out, const int32_t* __restrict__ lens,
                                                     int scale) {
-    extern __shared__ __attribute__((aligned(16))) float tl[];     // [C][7] weights, then [TAIL_T + 6][C + 4] rows
+    extern __shared__ __attribute__((aligned(16))) float tl[];     // [7][C] weights, then [TAIL_T + 6][C + 4] rows
     const int CS = C + 4, C4 = C / 4;
     float* wl = tl;
     float* rows = tl + ((C * 7 + 3) & ~3);
     const int b = blockIdx.y, t0 = blockIdx.x * TAIL_T;
     const int len = lens ? min(lens[b] * scale, T) : T;
-    for (int i = threadIdx.x; i < C * 7; i += TAIL_T) wl[i] = w[i];
+    for (int i = threadIdx.x; i < C * 7; i += TAIL_T) {            // w [C][7] -> [7][C]
+        const int c = i / 7, k = i - c * 7;
+        wl[k * C + c] = w[i];
+    }
     const float4* src = reinterpret_cast<const float4*>(s + (size_t)b * T * C);
-    const int nrow = TAIL_T + 6;
-    for (int i = threadIdx.x; i < nrow * C4; i += TAIL_T) {
-        const int r = i / C4, c4 = i - r * C4;
-        const int u = t0 - 3 + r;
-        const float4 v = (u >= 0 && u < len) ? src[(size_t)u * C4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(rows + r * CS + 4 * c4) = v;
+    const int nrow = TAIL_T + 6, total = nrow * C4;
+    // staging in batches of TAIL_NB loads per thread, all issued before the first LDS store: one
+    // load in flight per thread (load -> store -> next load) made the kernel a chain of ~25 memory
+    // round trips per workgroup (1.3 TB/s)
+    constexpr int TAIL_NB = ZK_TAIL_NB;
+    for (int i0 = threadIdx.x; i0 < total; i0 += TAIL_T * TAIL_NB) {
+        float4 v[TAIL_NB];
+#pragma unroll
+        for (int j = 0; j < TAIL_NB; ++j) {
+            const int i = i0 + j * TAIL_T;
+            const int r = i / C4, c4 = i - r * C4;
+            const int u = t0 - 3 + r;
+            v[j] = (i < total && u >= 0 && u < len) ? src[(size_t)u * C4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < TAIL_NB; ++j) {
+            const int i = i0 + j * TAIL_T;
+            const int r = i / C4, c4 = i - r * C4;
+            if (i < total) *reinterpret_cast<float4*>(rows + r * CS + 4 * c4) = v[j];
+        }
     }
     __syncthreads();
     const int t = t0 + threadIdx.x;
     if (t >= T) return;
-    float acc = 0.f;
+    // four independent accumulation chains (channel c mod 4), each weight quad one broadcast
+    // ds_read_b128: the single dependent chain with a scalar LDS weight read per FMA left one
+    // wave per SIMD waiting on LDS latency (1.3 TB/s on a streaming kernel)
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     for (int k = 0; k < 7; ++k) {
         const int u = t + k - 3;
         if (u < 0 || u >= len) continue;
         const float* row = rows + (threadIdx.x + k) * CS;
+        const float* wk = wl + k * C;
+#pragma unroll 4
         for (int c = 0; c < C; c += 4) {
             const float4 v = *reinterpret_cast<const float4*>(row + c);
-            acc = fmaf(wl[(c + 0) * 7 + k], v.x, acc);
-            acc = fmaf(wl[(c + 1) * 7 + k], v.y, acc);
-            acc = fmaf(wl[(c + 2) * 7 + k], v.z, acc);
-            acc = fmaf(wl[(c + 3) * 7 + k], v.w, acc);
+            const float4 q = *reinterpret_cast<const float4*>(wk + c);
+            a0 = fmaf(q.x, v.x, a0);
+            a1 = fmaf(q.y, v.y, a1);
+            a2 = fmaf(q.z, v.z, a2);
+            a3 = fmaf(q.w, v.w, a3);
         }
     }
+    const float acc = (a0 + a1) + (a2 + a3);
     out[(size_t)b * T + t] = (t < len) ? tanhf(__fadd_rn(acc, bias[0])) : 0.f;
 }
 
