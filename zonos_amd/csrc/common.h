@@ -20,6 +20,14 @@ ZK_DEV int32_t ld_word(const int32_t* p) {
     return __hip_atomic_load(p != nullptr ? p : &zk_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 ZK_DEV int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// The same word by a scalar load issued exactly here (inline asm: hipcc can neither hoist it above
+// the loads before it nor turn it into a vector load) and waited for at once.
+ZK_DEV int32_t ld_word_here(const int32_t* p) {
+    const int32_t* q = p != nullptr ? p : &zk_zero_word;
+    int32_t v;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(q) : "memory");
+    return v;
+}
 // Use of loaded registers on a kernel's early-exit path: without a use there, hipcc sinks the
 // loads into the path that consumes them, i.e. below the exit test, which then waits for the
 // step word before the first data load is issued.

@@ -274,7 +274,8 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
                                                            int wch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // (the skip word is tested first here: deferring the test behind the first loads, as k_gemv_f
-    // does, measured 0.3-0.4 us slower per launch at c3, profiles/r3s2_skip_defer_ab.txt)
+    // does, measured 0.3-1.2 % slower per c3 step with a vector or a scalar load of the word,
+    // profiles/r3s2_skip_defer_ab.txt)
     if (skip && *skip) return;
     int bx, bz;
     ws_tile(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x, gridDim.z, bx, bz);     // gridDim.y == 1
@@ -512,7 +513,6 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
                                                     float* __restrict__ Cpart, bf16_t* __restrict__ Cout,
                                                     const int32_t* skip) {
     __shared__ __attribute__((aligned(16))) f32x4 red[4][NTW][64];
-    const int sk = ld_word(skip);                           // tested once the prefetch is in flight
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int split = blockIdx.z;
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
     for (int p = 0; p < PF; ++p)
         if (p < KS) issue(p, p);
     __builtin_amdgcn_sched_barrier(0);
-    if (uni(sk)) {
+    if (ld_word_here(skip)) {                                  // tested once the prefetch is in flight
 #pragma unroll
         for (int p = 0; p < PF; ++p)
             if (p < KS) {
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     static_assert(!MRG || XR == 2, "merge prologue: M <= 2");
     __shared__ __attribute__((aligned(16))) uint4 xs[XS ? XR * GF_XS / 8 : 1];
     __shared__ __attribute__((aligned(16))) f32x4 red[NW][NTW][64];
-    const int sk = ld_word(skip);              // tested once the weight prefetch is in flight
+
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int nt0 = HALF ? (blockIdx.x >> 1) : blockIdx.x * NTW;    // first 16-column tile
@@ -737,7 +737,9 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
         if (p < NL) issue(p, p);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (uni(sk)) {                                      // every load above is in bounds; nothing written yet
+    // the skip word: a scalar load issued here, after the prologue loads and the weight prefetch
+    // (every load above is in bounds; nothing is written yet)
+    if (ld_word_here(skip)) {
         // (the prologue / epilogue loads too: sunk below this test they would queue behind the
         // weight prefetch and drain it when waited for)
 #pragma unroll
