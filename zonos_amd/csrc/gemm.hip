@@ -239,7 +239,12 @@ constexpr int WS_NLD = ZK_WS_NLD;            // loader waves (each moves 1/WS_NL
 #define ZK_WS_NT 1
 #endif
 constexpr int WS_LDSPF = 1;      // chunks published ahead of the one being multiplied
-constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave
+constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave: the SwiGLU fc1 (mode 1)
+#ifndef ZK_WS_PF0
+#define ZK_WS_PF0 3
+#endif
+constexpr int WS_PF0 = ZK_WS_PF0; // ... and the split-K slab GEMMs (mode 0): 3 measured faster for the
+                                  // in_proj / out_proj / fc2 shapes, 4 for fc1 (profiles/r3s2_gemm_pf_ab.txt)
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
 
 
@@ -1011,9 +1016,9 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
 #define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
     do {                                                                                                          \
         if (lds > 65536)                                                                                          \
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, WS_PF, MT_, NCW>),          \
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW>),          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
-        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, WS_PF, MT_, NCW>), g, dim3(64 * (NCW + WS_NLD)), lds,          \
+        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW>), g, dim3(64 * (NCW + WS_NLD)), lds,          \
                            (hipStream_t)stream,                                                                   \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
                            skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks);              \
