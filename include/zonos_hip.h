@@ -274,7 +274,8 @@ int zk_decode_step(const zk_step_desc* d, void* stream);
  * 2B*S positions (split-K 1, causal prefill attention filling the KV cache), the heads on the
  * last position, the first sample (model.py:304: no bias, no penalty) and the first frame write.
  * S = Lc + P + 1; q: bf16 [2B*S][H*hd] scratch; x / xn / y / h / part sized for 2B*S rows.
- * The loop state (st.scal, eos_mode, ...) is initialised by the host afterwards (model.py:316-342). */
+ * The loop state (st.scal, eos_mode, ...) is initialised by the host afterwards (model.py:316-342).
+ * Fails (-1, before any launch) unless smax >= Lc + st.Ld, the context of the last decode step. */
 int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P, void* q, void* stream);
 
 /* ------------------------------------------------------------------ hybrid decode step
@@ -516,6 +517,14 @@ int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_inner, int nh
                   void* conv_state_b, const int32_t* pos_dev, void* ssm_state, void* ssm_state_b,
                   const float* A, const float* dt_bias, const float* D, float* yz, const int32_t* skip,
                   void* stream);
+/* zk_mamba_step computed by the per-(head, row) kernel instead of the grouped one: same arguments,
+ * same results (bit for bit, or within 1 bf16 ulp of y where the C.h row sum is reduced in another
+ * order). The verification twin of zk_mamba_step; not on the decode path. */
+int zk_mamba_step_per_head(const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
+                           int d_state, const float* conv_w, const float* conv_b, void* conv_state_a,
+                           void* conv_state_b, const int32_t* pos_dev, void* ssm_state, void* ssm_state_b,
+                           const float* A, const float* dt_bias, const float* D, float* yz, const int32_t* skip,
+                           void* stream);
 /* prefill over S positions per row: zx = in_proj output fp32 [R*S][cols] (split 1); xc_scratch
  * bf16 [R*S][conv_dim]; conv_state receives the last 4 inputs (the buffer the first decode step
  * reads); ssm_state receives the final state (bf16; with double-buffered decode states, the

@@ -50,6 +50,23 @@ def test_argument_validation_without_gpu(lib):
     assert b"zk_gemm_bf16" in lib.zk_last_error()
 
 
+def test_prefill_rejects_short_kv_cache_without_gpu(lib):
+    """zk_prefill / zk_hybrid_prefill refuse a descriptor whose KV cache (smax keys) is shorter than
+    the context of the last decode step (Lc + Ld), before any launch: the decode attention's context
+    clamp is then only ever reached by no-op launches after the last step."""
+    import ctypes as C
+
+    from zonos_amd import _lib
+    lays = (_lib.StepLayer * 1)()
+    d = _lib.StepDesc()
+    d.B, d.n_layer, d.d_model, d.smax, d.layers = 1, 1, 64, 256, C.cast(lays, C.c_void_p)
+    d.st.Ld, d.st.K, d.st.V = 250, 9, 1026
+    buf = C.create_string_buffer(16)
+    lib.zk_last_error.restype = C.c_char_p
+    assert lib.zk_prefill(C.byref(d), buf, 10, 0, buf, None) != 0      # 10 + 250 > 256
+    assert b"KV cache" in lib.zk_last_error()
+
+
 def test_split_selection_batch_invariant():
     from zonos_amd.engine import _split_for
     for N, K in ((3072, 2048), (2048, 2048), (2048, 8192), (9234, 2048)):

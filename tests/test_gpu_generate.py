@@ -260,3 +260,21 @@ def test_sampling_loggers_do_not_change_codes(capsys):
     before = [l for l in out if l.startswith("Before Batch 0, Codebook 0 | Top 5:")]
     after = [l for l in out if l.startswith("After  Batch 0, Codebook 0 | Top 5:")]
     assert len(before) == len(after) >= c["max_new"], (len(before), out[:3])
+
+
+def test_root_debug_eos_message_keeps_multistep_polls(caplog):
+    """A root logger at DEBUG (logging.basicConfig(level=DEBUG)) gets model.py:381's EOS message with
+    the detection offset, without forcing one graph launch per step: the messages recovered at the
+    boundaries of multi-step polls equal those of a one-step-per-poll run, and the codes are unchanged."""
+    import logging
+    c = load_gen_case("copy_eos")
+    eng = _engine(c["W"], c["cfg"])
+    args = (c["cond"].cuda(), c["prefix"].cuda(), c["max_new"], 2.0, c["B"], c["sp"])
+    msgs, outs = [], []
+    with caplog.at_level(logging.DEBUG):
+        for poll in (1, 16):
+            caplog.clear()
+            outs.append(eng.generate(*args, seed=c["seed"], poll_every=poll))
+            msgs.append([r.getMessage() for r in caplog.records if r.getMessage().startswith("Detected EOS")])
+    assert msgs[0] and msgs[0] == msgs[1], msgs
+    assert all(torch.equal(a, b) for a, b in zip(*outs))

@@ -141,20 +141,20 @@ def test_mamba_step_grouped_equals_per_head(hp, ds, nh, R, gs, pos, monkeypatch)
     s = stream_ptr()
     outs = []
     for grouped, pingpong in (("0", False), ("1", False), ("1", True), ("0", True)):
-        monkeypatch.setenv("ZK_MAMBA_GROUPED", grouped)
+        fn = "zk_mamba_step" if grouped == "1" else "zk_mamba_step_per_head"
         ca, cbuf = conv0.to(DEV), conv0.to(DEV)
         ssm = ssm0.to(DEV)
         yz = torch.full((R, di), float("nan"), device=DEV)
         if pingpong:       # {a, b}: the step at position pos reads (pos & 1) and writes the other
             other = torch.full_like(ssm, float("nan"))
             sa, sb = (other, ssm) if pos & 1 else (ssm, other)
-            call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
+            call(fn, ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
                  ptr(sa), ptr(sb), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
             torch.cuda.synchronize()
             assert torch.equal(ssm.cpu(), ssm0), "ping-pong read buffer modified"
             ssm = other
         else:
-            call("zk_mamba_step", ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
+            call(fn, ptr(parts), gs, R, di, nh, hp, ds, ptr(cw), ptr(cb), ptr(ca), ptr(cbuf), ptr(posd),
                  ptr(ssm), None, ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, s)
             torch.cuda.synchronize()
         outs.append((ca.cpu(), cbuf.cpu(), ssm.cpu(), yz.cpu()))

@@ -113,6 +113,38 @@ def test_generate_sharded_gloo_world2():
     assert all(ok for _, ok in res), res
 
 
+def _default_args_worker(rank, world, port, q):
+    """The documented call: no seed, no coll_device, and B < world so rank 1's shard is empty."""
+    from zonos_amd.distributed import collective_device, generate_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(99 + rank)
+    B = 1
+    cond, prefix = _global_inputs(B)
+    got = generate_sharded(StubEngine(), cond, prefix, 8, 2.0, B)
+    ref = StubEngine().generate(cond, prefix, 8, 2.0, B, {}, seed=0, row_base=0)
+    ok = len(got) == 1 and got[0].shape == ref[0].shape and collective_device() == torch.device("cpu")
+    q.put((rank, ok, [tuple(c.shape) for c in got], int(got[0][0, 0]) if got else None))
+    dist.destroy_process_group()
+
+
+def test_generate_sharded_default_args_empty_shard():
+    """seed=None, coll_device=None, B=1 over 2 ranks (one empty shard) -- the collectives
+    pick the group's device on every rank and both ranks return the same codes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_default_args_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] for r in res), res
+    assert res[0][3] == res[1][3], res
+
+
 def test_generate_sharded_single_process():
     from zonos_amd.distributed import generate_sharded
     cond, prefix = _global_inputs(4)

@@ -110,6 +110,7 @@ _SIGS = {
     "zk_hybrid_prefill": [C.POINTER(HybridDesc), P, I, I, P, P],
     "zk_dac_decode": [C.POINTER(DacDesc), P, I, I, P, P, C.c_size_t, P, P],
     "zk_mamba_step": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "zk_mamba_step_per_head": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "zk_mamba_prefill": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "zk_gated_rmsnorm": [P, I, I, P, F, P, P, P],
     "zk_attn_prefill": [P, P, P, I, I, I, I, I, I, P, P],

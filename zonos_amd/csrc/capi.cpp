@@ -209,6 +209,13 @@ extern "C" int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P
         zk_set_error("zk_prefill: bad arguments");
         return -1;
     }
+    // The last decode step attends over Lc + Ld keys (S = Lc + P + 1 after the prefill, plus
+    // Ld - (P + 1) steps, model.py:335-345). The decode attention clamps its context to smax so a
+    // no-op launch after the last step stays in bounds; a real step must never need that clamp.
+    if (Lc + d->st.Ld > d->smax) {
+        zk_set_error("zk_prefill: KV cache of %d keys is shorter than Lc + Ld = %d", d->smax, Lc + d->st.Ld);
+        return -1;
+    }
     const int K = d->st.K, V = d->st.V, B = d->B, R = 2 * B, S = Lc + P + 1, M = R * S;
     const int D = d->d_model, H = d->n_heads, Hk = d->n_kv, hd = d->head_dim, Fd = d->d_ff;
     const int Nqkv = (H + 2 * Hk) * hd;
@@ -343,6 +350,10 @@ extern "C" int zk_hybrid_decode_step(const zk_hybrid_desc* d, void* stream) {
 extern "C" int zk_hybrid_prefill(const zk_hybrid_desc* d, const void* cond, int Lc, int P, void* q, void* stream) {
     if (!hybrid_ok(d) || cond == nullptr || q == nullptr || Lc < 0 || P < 0) {
         zk_set_error("zk_hybrid_prefill: bad arguments");
+        return -1;
+    }
+    if (Lc + d->st.Ld > d->smax) {     // as zk_prefill: no real step may need the attention's clamp
+        zk_set_error("zk_hybrid_prefill: KV cache of %d keys is shorter than Lc + Ld = %d", d->smax, Lc + d->st.Ld);
         return -1;
     }
     const int K = d->st.K, V = d->st.V, B = d->B, R = 2 * B, S = Lc + P + 1, D = d->d_model;

@@ -680,12 +680,10 @@ int launch_conv(long ntiles, size_t lds, hipStream_t st, const uint16_t* in, int
     if (lds > 65536)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
-    static int ncu = 0;
-    if (ncu == 0) {
-        int dev = 0;
-        ZK_HIP(hipGetDevice(&dev));
-        ZK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
+    // the current device's CU count (queried per call: a process may drive several devices)
+    int dev = 0, ncu = 0;
+    ZK_HIP(hipGetDevice(&dev));
+    ZK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     int occ = 0;
     ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kern), NT, lds));
     ZK_REQUIRE(occ >= 1, "zk_dac_conv_cl: kernel does not fit a CU (LDS %zu)", lds);

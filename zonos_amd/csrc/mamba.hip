@@ -449,19 +449,18 @@ __global__ __launch_bounds__(MB_THREADS) void k_gated_norm(const float* __restri
 #define ZK_MB_DISPATCH(HP_, DS_, CALL)                                                     \
     if (hp == HP_ && ds == DS_) { CALL(HP_, DS_); handled = true; }
 
-extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
-                             int d_state, const float* conv_w, const float* conv_b, void* conv_state_a,
-                             void* conv_state_b, const int32_t* pos_dev, void* ssm_state, void* ssm_state_b,
-                             const float* A, const float* dt_bias, const float* D, float* yz, const int32_t* skip,
-                             void* stream) {
+namespace {
+
+// grouped = true: ZK_MB_HG heads per workgroup (default 1, the fastest measured; B/C conv once per
+// group), in_proj splits 1 / 2 / 4. grouped = false: one workgroup per (head, row), any split.
+int mamba_step(bool grouped, const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
+               int d_state, const float* conv_w, const float* conv_b, void* conv_state_a, void* conv_state_b,
+               const int32_t* pos_dev, void* ssm_state, void* ssm_state_b, const float* A, const float* dt_bias,
+               const float* D, float* yz, const int32_t* skip, void* stream) {
     const int hp = headdim, ds = d_state;
     ZK_REQUIRE(gemm_nsplit >= 1 && gemm_nsplit <= MB_MAXGS, "zk_mamba_step: gemm_nsplit=%d", gemm_nsplit);
     ZK_REQUIRE(nheads * headdim == d_inner, "zk_mamba_step: nheads*headdim != d_inner");
     bool handled = false;
-    // grouped kernel: ZK_MB_HG heads per workgroup (default 1, the fastest measured; B/C conv once per
-    // group), in_proj splits 1 / 2 / 4
-    const char* ge = getenv("ZK_MAMBA_GROUPED");   // "0": per-head kernel (A/B knob; read per launch call,
-    const bool grouped = !(ge && ge[0] == '0');    // graph replays do not call here)
     if (grouped && nheads % ZK_MB_HG == 0 && (gemm_nsplit == 1 || gemm_nsplit == 2 || gemm_nsplit == 4)) {
 #define ZK_MB_STEPG(HP_, DS_)                                                                                       \
     do {                                                                                                           \
@@ -499,6 +498,26 @@ extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_in
     ZK_REQUIRE(handled, "zk_mamba_step: (headdim %d, d_state %d) not instantiated", hp, ds);
     ZK_CHECK_LAUNCH("zk_mamba_step");
     return 0;
+}
+
+}  // namespace
+
+extern "C" int zk_mamba_step(const float* part, int gemm_nsplit, int R, int d_inner, int nheads, int headdim,
+                             int d_state, const float* conv_w, const float* conv_b, void* conv_state_a,
+                             void* conv_state_b, const int32_t* pos_dev, void* ssm_state, void* ssm_state_b,
+                             const float* A, const float* dt_bias, const float* D, float* yz, const int32_t* skip,
+                             void* stream) {
+    return mamba_step(true, part, gemm_nsplit, R, d_inner, nheads, headdim, d_state, conv_w, conv_b, conv_state_a,
+                      conv_state_b, pos_dev, ssm_state, ssm_state_b, A, dt_bias, D, yz, skip, stream);
+}
+
+extern "C" int zk_mamba_step_per_head(const float* part, int gemm_nsplit, int R, int d_inner, int nheads,
+                                      int headdim, int d_state, const float* conv_w, const float* conv_b,
+                                      void* conv_state_a, void* conv_state_b, const int32_t* pos_dev, void* ssm_state,
+                                      void* ssm_state_b, const float* A, const float* dt_bias, const float* D,
+                                      float* yz, const int32_t* skip, void* stream) {
+    return mamba_step(false, part, gemm_nsplit, R, d_inner, nheads, headdim, d_state, conv_w, conv_b, conv_state_a,
+                      conv_state_b, pos_dev, ssm_state, ssm_state_b, A, dt_bias, D, yz, skip, stream);
 }
 
 extern "C" int zk_mamba_prefill(const float* zx, int R, int S, int d_inner, int nheads, int headdim, int d_state,

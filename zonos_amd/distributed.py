@@ -19,11 +19,23 @@ def shard(global_batch: int, world: int, rank: int) -> tuple[int, int]:
     return start, local
 
 
+def collective_device(group=None) -> torch.device:
+    """The device a collective of ``group`` runs on: the current GPU for an nccl (RCCL) group,
+    which has no CPU backend, else the CPU (gloo). Every rank must pass tensors on the same kind of
+    device, whatever its shard holds, so this depends on the group only."""
+    backend = str(dist.get_backend(group)).lower()
+    if "nccl" in backend:
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def gather_codes(codes: list, device=None, group=None) -> list:
     """All-gather a list of int [9, T_i] code tensors from every rank (rank order = global
-    utterance order). Codes travel as int32 (values <= 1025) padded to the max length."""
+    utterance order). Codes travel as int32 (values <= 1025) padded to the max length.
+    ``device`` None picks the group's collective device (`collective_device`), also on a rank
+    whose shard is empty."""
     world = dist.get_world_size(group)
-    device = device or (codes[0].device if codes else torch.device("cpu"))
+    device = torch.device(device) if device is not None else collective_device(group)
     n = torch.tensor([len(codes)], device=device)
     ns = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(ns, n, group=group)
@@ -70,6 +82,8 @@ def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_code
       global [B, 9, P]); with ``local_input=True`` they already hold only this rank's rows
       ([2b, Lc, D] / [b, 9, P], b = the rank's share).
     * ``seed`` None draws one seed on rank 0 from torch's generator and broadcasts it.
+    * ``coll_device`` None runs the collectives on the group's device (`collective_device`: the
+      current GPU under nccl, the CPU under gloo).
     * No collective touches the decode; with ``gather`` one all_gather of the int32 codes returns
       the global list (utterance order) on every rank, else the rank's own list;
       ``return_local`` returns (the rank's own list on its device, the gathered list).
@@ -79,9 +93,11 @@ def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_code
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if world > 1 else 0
     row_base, local = shard(batch_size, world, rank)
+    if world > 1 and coll_device is None:
+        coll_device = collective_device(group)
     if world > 1 and seed is None:
         s = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64) if rank == 0 else torch.zeros(1, dtype=torch.int64)
-        s = s.to(coll_device or "cpu")
+        s = s.to(coll_device)
         dist.broadcast(s, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         seed = int(s.item())
     elif seed is None:

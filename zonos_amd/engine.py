@@ -452,7 +452,13 @@ class HipDecoder(HipBackbone):
             call("zk_eos_step", C_ref(st), 1, P + 1, stream)
         if _after_prefill is not None:      # test hook (teacher forcing of the first frame)
             _after_prefill(ws["delayed"][..., P + 1:P + 2])
-        logdbg = zsampling.debug_enabled() or logging.getLogger().isEnabledFor(logging.DEBUG)
+        # Debug logging. The sampler statistics need the logits of every step (one step per poll);
+        # model.py:381's EOS message on the root logger only needs the steps where a row entered EOS
+        # mode, which are recovered at poll boundaries from the eos_mode / steps_after words
+        # (`_log_new_eos`), so a root logger at DEBUG level keeps multi-step polls (<= 6 steps, the
+        # EOS hold-off, so the detection offset is exact).
+        logdbg = zsampling.debug_enabled()
+        eosdbg = not logdbg and logging.getLogger().isEnabledFor(logging.DEBUG)
         if zsampling.debug_enabled():       # the reference's sampler statistics (sampling.py:287-322)
             zsampling.log_sampling_stats(
                 zsampling.engine_logits_row(ws["dbg"][0, 0], True, False, EOS, force_full_length), spd, None, 1.0, EOS)
@@ -472,6 +478,9 @@ class HipDecoder(HipBackbone):
 
         # ---- decode loop (model.py:345-432)
         per_poll = 1 if (callback is not None or trace is not None or logdbg) else max(1, poll_every)
+        if eosdbg:
+            per_poll = min(per_poll, 6)
+            eos_prev = ws["eos_mode"].cpu()
         graph = None
         if use_graph and trace is None:
             graph = self._capture(ws, B, st, sp, stream)
@@ -493,6 +502,8 @@ class HipDecoder(HipBackbone):
             if trace is not None:
                 trace["logits"].append(ws["dbg"].clone())
             scal = ws["scal"].cpu()
+            if eosdbg:
+                eos_prev = self._log_new_eos(ws, eos_prev, int(scal[0]) - 1)
             if progress is not None:
                 progress.update(n)
             if callback is not None:
@@ -510,6 +521,23 @@ class HipDecoder(HipBackbone):
             trace["delayed"] = ws["delayed"].clone()
             trace["offset"] = offset
         return finalize(ws["delayed"], offset, P, stream)
+
+    def _log_new_eos(self, ws, eos_prev, off_last):
+        """model.py:381's message for the rows that entered EOS mode during the last poll.
+        A row detected at offset o has had its hold-off counter (6 at detection, model.py:384)
+        decremented once per later step (model.py:360-362), so o = off_last - 6 + steps_after
+        while the poll is at most 6 steps long."""
+        eos1 = ws["eos_mode"].cpu()
+        new = ((eos1 != 0) & (eos_prev == 0)).nonzero(as_tuple=True)[0].tolist()
+        if new:
+            sa = ws["steps_after"].cpu()
+            by_off = {}
+            for r in new:
+                by_off.setdefault(off_last - 6 + int(sa[r]), []).append(r)
+            for off in sorted(by_off):
+                logging.debug(f"Detected EOS in codebook 0 for samples: {by_off[off]} at offset {off}. "
+                              "Resampling with -torch.inf.")
+        return eos1
 
     def _log_step(self, ws, spd, pre, force_full_length):
         """Debug logging of one executed decode step (per_poll = 1): the sampler statistics of
