@@ -96,7 +96,9 @@ class HybridCfg:
     def to_zonos_config(self) -> dict:
         return {
             "backbone": {"d_model": self.d_model, "d_intermediate": 0, "attn_mlp_d_intermediate": self.d_ff,
-                         "n_layer": self.n_layer, "ssm_cfg": {"layer": "Mamba2"},
+                         "n_layer": self.n_layer, "ssm_cfg": {"layer": "Mamba2", "d_state": self.d_state, "d_conv": self.d_conv,
+                                                                 "expand": self.expand, "headdim": self.headdim,
+                                                                 "ngroups": self.ngroups},
                          "attn_layer_idx": list(self.attn_layer_idx),
                          "attn_cfg": {"causal": True, "num_heads": self.n_heads, "num_heads_kv": self.n_kv,
                                       "rotary_emb_dim": self.head_dim, "qkv_proj_bias": False,

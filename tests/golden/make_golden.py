@@ -449,6 +449,44 @@ def make_dac_fixtures():
                             cfg=np.array([c.hidden_size, c.decoder_hidden_size, *c.upsampling_ratios]))
 
 
+def _q16(w: torch.Tensor):
+    """int16 quantisation of a waveform, scale = max|w| / 32767: the rounding error's RMS is
+    scale / sqrt(12) (~3e-6 at the fixture's amplitude), far below the 1e-4 RMS parity bar."""
+    scale = max(float(w.abs().max()), 1e-30) / 32767.0
+    return torch.round(w / scale).to(torch.int16).numpy(), np.float64(scale)
+
+
+def make_dac_long_fixture():
+    """A 44.1 kHz DacModel decode long enough that the channels-last convs stream several tiles per
+    persistent workgroup (the c3 regime): 2 ragged rows of 600 / 437 frames (307,200 samples), the
+    short row also decoded alone. Waveforms are stored int16-quantised with their scales (_q16)."""
+    c, seed, T = dac_ref.DAC_44KHZ, 0, (600, 437)
+    W = dac_ref.make_dac_weights(c, seed=seed)
+    hf = DacModel(DacConfig(sampling_rate=44100, hidden_size=c.hidden_size,
+                            decoder_hidden_size=c.decoder_hidden_size, upsampling_ratios=list(c.upsampling_ratios),
+                            n_codebooks=c.n_codebooks, codebook_size=c.codebook_size, codebook_dim=c.codebook_dim))
+    sd = hf.state_dict()
+    for k, v in W.items():
+        sd[k] = v
+    hf.load_state_dict(sd)
+    hf.eval()
+    g = torch.Generator().manual_seed(seed + 300)
+    codes = torch.randint(0, c.codebook_size, (2, c.n_codebooks, T[0]), generator=g)
+    short = codes[1:, :, :T[1]].clone()
+    with torch.no_grad():
+        wav_b = hf.decode(audio_codes=codes).audio_values.unsqueeze(1).float()   # autoencoder.py:47 (CPU)
+        wav_s = hf.decode(audio_codes=short).audio_values.unsqueeze(1).float()
+    o_s = dac_ref.decode(W, c, short)                    # the oracle on the short row (the long one: same code)
+    es = (o_s - wav_s).abs().max().item()
+    print(f"[dac_44k_long] rms={wav_b.pow(2).mean().sqrt().item():.4f} oracle max|d| short={es:.2e}")
+    assert es < 1e-5
+    qb, sb = _q16(wav_b)
+    qs, ss = _q16(wav_s)
+    np.savez_compressed(os.path.join(HERE, "dac_44k_long.npz"), codes=codes.numpy().astype(np.int16),
+                        wav_q=qb, wav_scale=sb, wav_short_q=qs, wav_short_scale=ss, short_len=np.int32(T[1]),
+                        seed=np.int64(seed), wsum=np.array(wsum(W)))
+
+
 ENC_DAC = dac_ref.DacCfg(hidden_size=64, decoder_hidden_size=64, upsampling_ratios=(8, 8, 4, 2),
                          encoder_hidden_size=32, downsampling_ratios=(2, 4, 8, 8))
 
@@ -533,6 +571,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "enc":
         make_dac_encoder_fixture()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "dac_long":
+        make_dac_long_fixture()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "cond":
         make_cond_fixtures()
         sys.exit(0)
@@ -548,5 +589,6 @@ if __name__ == "__main__":
     make_copy_fixtures()
     make_full_fixtures()
     make_dac_fixtures()
+    make_dac_long_fixture()
     make_dac_encoder_fixture()
     make_cond_fixtures()

@@ -56,6 +56,14 @@ FULL_CASES = {
 FULL_SEED = 1234
 
 
+# c5: the hybrid at the benchmark workload (bench.py --model hybrid: B = 64, Lc = 400, P = 10, 2580
+# tokens), three utterances (first, middle, last of the batch), logits from the first steps to the
+# last attention contexts (~2980) -- restatement-generated (tests/golden/make_hybrid_golden.py)
+HYBRID_C5 = dict(B=64, Lc=400, P=10, T=2580, utts=(0, 37, 63), w_seed=0, cond_seed=1, prefix_seed=3, hist_seed=7,
+                 seed=FULL_SEED,
+                 logit_steps=(0, 1, 2, 256, 768, 1290, 1291, 1792, 2304, 2568, 2569, 2570))
+
+
 def forced_history(B: int, P: int, T: int, prefix, seed: int = 7) -> torch.Tensor:
     """Delayed codes [B, 9, T+9] of a seeded random history after the prefix (teacher forcing)."""
     g = torch.Generator().manual_seed(seed)

@@ -19,7 +19,7 @@ def test_zonos_import_surface():
     import zonos_amd.autoencoder
     import zonos_amd.model
     assert Zonos is zonos_amd.model.Zonos and DACAutoencoder is zonos_amd.autoencoder.DACAutoencoder
-    assert DEFAULT_BACKBONE_CLS is BACKBONES["hip"]
+    assert DEFAULT_BACKBONE_CLS is BACKBONES["hip_hybrid"]
     assert "transformer" in BACKBONES["hip"].supported_architectures
     assert isinstance(DEFAULT_DEVICE, torch.device) and find_multiple(1025, 8) == 1032
     assert "en-us" in supported_language_codes
@@ -57,3 +57,40 @@ def test_pad_weight_matches_reference_branches():
     assert torch.equal(lin.weight[:1025], w0) and not lin.weight[1025].any()
     with pytest.raises(ValueError):
         pad_weight_(torch.nn.Conv1d(2, 2, 1), 8)
+
+
+def test_hybrid_backbone_plugin_parameter_layout_and_registry():
+    """HipHybridBackbone's state dict = mamba_ssm's Block / Mamba2 / MHA names and shapes (the
+    restatement's weight_shapes), the registry mirrors the reference's (hybrid-capable class first,
+    its keys as aliases), and a transformer config builds the transformer blocks."""
+    from oracle import hybrid_ref
+    from zonos.backbone import BACKBONES
+    from zonos.config import BackboneConfig
+    from zonos.model import DEFAULT_BACKBONE_CLS
+    c = hybrid_ref.HybridCfg(d_model=256, n_layer=4, attn_layer_idx=(2,), n_heads=2, n_kv=1, d_ff=512, d_state=64,
+                             headdim=32)
+    bb = BACKBONES["mamba_ssm"](BackboneConfig(**c.to_zonos_config()["backbone"]))
+    got = {k: tuple(v.shape) for k, v in bb.state_dict().items()}
+    exp = {k[len("backbone."):]: v for k, v in hybrid_ref.weight_shapes(c).items() if k.startswith("backbone.")}
+    assert got == exp
+    assert DEFAULT_BACKBONE_CLS.supported_architectures == ["transformer", "hybrid"]
+    assert BACKBONES["torch"].supported_architectures == ["transformer"]
+    tb = BACKBONES["mamba_ssm"](BackboneConfig(**TINY.to_zonos_config()["backbone"]))
+    assert {k: tuple(v.shape) for k, v in tb.state_dict().items()} == \
+        {k[len("backbone."):]: v for k, v in zonos_ref.weight_shapes(TINY).items() if k.startswith("backbone.")}
+
+
+def test_from_local_backbone_selector_errors(tmp_path):
+    """from_local(backbone=...) as the reference (model.py:69-70): an unknown key raises KeyError, a
+    class without the checkpoint's architecture raises -- before any weight is read."""
+    import json
+
+    import pytest
+    from oracle import hybrid_ref
+    from zonos.model import Zonos
+    cfg = tmp_path / "config.json"
+    cfg.write_text(json.dumps(hybrid_ref.HybridCfg(n_layer=4, attn_layer_idx=(2,)).to_zonos_config()))
+    with pytest.raises(KeyError):
+        Zonos.from_local(str(cfg), str(tmp_path / "missing.safetensors"), backbone="nope")
+    with pytest.raises(ValueError, match="hybrid"):
+        Zonos.from_local(str(cfg), str(tmp_path / "missing.safetensors"), backbone="torch")

@@ -121,3 +121,75 @@ def test_tail_conv_matches_fp32_conv(C):
     torch.cuda.synchronize()
     err = (out.cpu().double() - ref).abs().max().item()
     assert err < 1e-5, err
+
+
+def _long():
+    from zonos_amd.autoencoder import DacSpec, HipDacDecoder
+    d = np.load(os.path.join(G, "dac_44k_long.npz"))
+    c = dac_ref.DAC_44KHZ
+    W = dac_ref.make_dac_weights(c, seed=int(d["seed"]))
+    dec = HipDacDecoder(DacSpec(c.hidden_size, c.decoder_hidden_size, c.upsampling_ratios), W, "cuda",
+                        precision="fp16")
+    codes = torch.from_numpy(d["codes"].astype(np.int64)).cuda()
+    wav = torch.from_numpy(d["wav_q"].astype(np.float32)) * float(d["wav_scale"])
+    wav_s = torch.from_numpy(d["wav_short_q"].astype(np.float32)) * float(d["wav_short_scale"])
+    return dec, d, codes, wav, wav_s
+
+
+def _tiles_per_workgroup(B, Qn, Cout, resid=False, nphase=1):
+    """Tiles each persistent workgroup of zk_dac_conv_cl streams at least (dac_cl.hip launch_conv:
+    grid = min(tiles, resident workgroups); the fat 12-wave form holds one workgroup per CU on
+    512-position tiles, the others at most two per CU on 128-position tiles)."""
+    nco = Cout // 32
+    FM = 4 if nco % 4 == 0 else 3 if nco % 3 == 0 else 2 if nco % 2 == 0 else 1
+    fat = not resid and nphase == 1 and FM <= 3
+    qt = 512 if fat else 128
+    ntiles = B * (-(-Qn // qt)) * (Cout // (32 * FM)) * nphase
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    return ntiles // (ncu * (1 if fat else 2))
+
+
+def test_dac_long_golden_multitile():
+    """The c3 regime: every decoder stage after the first streams >= 2 tiles per persistent
+    workgroup (tile carry-over of the loader rings, dac_cl.hip:148-160). fp16 decode of 2 x 600
+    frames vs the reference DacModel: RMS <= 1e-4 (north_star), both rows."""
+    dec, d, codes, wav, _ = _long()
+    # the stages' (rows, positions, channels): 8x at 768 ch, 64x at 384 (x4 tiles), 512x at 96
+    T = codes.shape[2]
+    assert _tiles_per_workgroup(2, 8 * T, 768, resid=True) >= 2
+    assert _tiles_per_workgroup(2, 64 * T, 384) >= 2
+    assert _tiles_per_workgroup(2, 512 * T, 96) >= 2 and _tiles_per_workgroup(2, 512 * T, 96, resid=True) >= 2
+    got = dec.decode_padded(codes).cpu()
+    assert got.shape == wav.shape
+    for b in range(2):
+        rms = (got[b] - wav[b]).pow(2).mean().sqrt().item()
+        assert rms <= 1e-4, (b, rms)
+    assert (got - wav).abs().max().item() < 2e-3
+
+
+def test_dac_long_ragged_row_bit_identical_and_golden():
+    """Ragged batch at the long size: the 437-frame row decoded beside the 600-frame one equals the
+    row decoded alone bit for bit, is zero past its length, and matches the reference's own decode
+    of that row (RMS <= 1e-4)."""
+    dec, d, codes, _, wav_s = _long()
+    L = int(d["short_len"])
+    lens = torch.tensor([codes.shape[2], L], dtype=torch.int32)
+    both = dec.decode_padded(codes, lens)
+    alone = dec.decode_padded(codes[1:2, :, :L].contiguous())
+    hop = dec.spec.hop_length
+    assert torch.equal(both[1, :, :L * hop], alone[0])
+    assert torch.count_nonzero(both[1, :, L * hop:]) == 0
+    rms = (alone[0].cpu() - wav_s[0]).pow(2).mean().sqrt().item()
+    assert rms <= 1e-4, rms
+
+
+def test_c_dac_decode_long_equals_python_sequence(monkeypatch):
+    """zk_dac_decode == the Python-issued launch sequence at the multi-tile size, ragged."""
+    from zonos_amd.autoencoder import HipDacDecoder
+    dec, d, codes, _, _ = _long()
+    lens = torch.tensor([codes.shape[2], int(d["short_len"])], dtype=torch.int32, device="cuda")
+    outs = []
+    for flag in (True, False):
+        monkeypatch.setattr(HipDacDecoder, "c_dac", flag)
+        outs.append(dec.decode_padded(codes, lens).cpu())
+    assert torch.equal(outs[0], outs[1])

@@ -46,9 +46,33 @@ CONV_CASES = [  # Cin, Cout, ks, dil, T, resid
 ]
 
 
-@pytest.mark.parametrize("Cin,Cout,ks,dil,T,use_resid", CONV_CASES)
+# More tiles than resident workgroups (each persistent workgroup streams >= 2 tiles through its
+# loader rings, dac_cl.hip:148-160): the fat 12-wave k7 form (96 / 192 channels, 512-position tiles,
+# one workgroup per CU), the residual 1x1 form and the FM = 4 k7 form (two per CU, 128 positions).
+MULTITILE_CASES = [
+    (96, 96, 7, 3, 120000, False),
+    (192, 192, 7, 1, 70000, False),
+    (96, 96, 1, 1, 60000, True),
+    (384, 384, 1, 1, 30000, True),
+    (1024, 1536, 7, 1, 4000, False),
+]
+
+
+def _min_tiles_per_wg(B, T, Cout, resid):
+    nco = Cout // 32
+    FM = 4 if nco % 4 == 0 else 3 if nco % 3 == 0 else 2 if nco % 2 == 0 else 1
+    fat = not resid and FM <= 3
+    qt = 512 if fat else 128
+    ntiles = B * (-(-T // qt)) * (Cout // (32 * FM))
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    return ntiles // (ncu * (1 if fat else 2))
+
+
+@pytest.mark.parametrize("Cin,Cout,ks,dil,T,use_resid", CONV_CASES + MULTITILE_CASES)
 def test_conv_cl_vs_torch(Cin, Cout, ks, dil, T, use_resid):
     L = _lib()
+    if T >= 4000:
+        assert _min_tiles_per_wg(3, T, Cout, use_resid) >= 2
     torch.manual_seed(Cin + Cout + ks + dil)
     dev = "cuda"
     B = 3
@@ -88,7 +112,8 @@ def test_conv_cl_vs_torch(Cin, Cout, ks, dil, T, use_resid):
     assert (s32 - s_ref).abs().max().item() < 2e-3 * max(1.0, s_ref.abs().max().item())
 
 
-@pytest.mark.parametrize("Cin,Cout,st,T", [(192, 96, 2, 70), (1536, 768, 8, 12), (384, 192, 4, 33)])
+@pytest.mark.parametrize("Cin,Cout,st,T", [(192, 96, 2, 70), (1536, 768, 8, 12), (384, 192, 4, 33),
+                                          (192, 96, 2, 40000), (768, 384, 4, 9000)])
 def test_convt_cl_vs_torch(Cin, Cout, st, T):
     L = _lib()
     torch.manual_seed(st + T)

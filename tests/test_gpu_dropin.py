@@ -81,11 +81,15 @@ def env(tmp_path_factory):
             os.environ[k] = v
 
 
-def test_from_local_checkpoint_reproduces_reference_codes(env):
+@pytest.mark.parametrize("backbone", [None, "torch", "mamba_ssm"])
+def test_from_local_checkpoint_reproduces_reference_codes(env, backbone):
+    """from_local with the reference's backbone selector (model.py:66-77): the default, the torch
+    backbone's key and mamba_ssm's (whose class supports the transformer architecture too)."""
     from zonos.model import Zonos
     c = env["case"]
     d = str(env["tmp"] / "ckpt")
-    model = Zonos.from_local(os.path.join(d, "config.json"), os.path.join(d, "model.safetensors"), device="cuda")
+    model = Zonos.from_local(os.path.join(d, "config.json"), os.path.join(d, "model.safetensors"), device="cuda",
+                             backbone=backbone)
     out = model.generate(c["cond"].cuda(), c["prefix"].cuda(), c["max_new"], 2.0, c["B"], c["sp"],
                          progress_bar=False, seed=c["seed"])
     assert [int(x.shape[1]) for x in out] == c["lens"].tolist()

@@ -86,6 +86,22 @@ def test_dac_golden(name):
     assert (got_s - torch.from_numpy(d["wav_short"][0])).abs().max().item() < 1e-5
 
 
+def test_dac_long_golden():
+    """dac_44k_long.npz (reference DacModel, 2 x 600 frames, int16-quantised): the oracle's decode of
+    the short row (437 frames) within the quantisation step, and the stored scales consistent."""
+    d = np.load(os.path.join(G, "dac_44k_long.npz"))
+    c = dac_ref.DAC_44KHZ
+    W = dac_ref.make_dac_weights(c, seed=int(d["seed"]))
+    assert wsum(W) == str(d["wsum"])
+    codes = torch.from_numpy(d["codes"].astype(np.int64))
+    L = int(d["short_len"])
+    ref_s = torch.from_numpy(d["wav_short_q"][0].astype(np.float32)) * float(d["wav_short_scale"])
+    with torch.no_grad():
+        got_s = dac_ref.decode_list(W, c, [codes[1, :, :L]])[0]
+    assert got_s.shape == ref_s.shape == (1, L * 512)
+    assert (got_s - ref_s).abs().max().item() <= 0.5 * float(d["wav_short_scale"]) + 1e-6
+
+
 def test_dac_encoder_golden():
     """oracle DAC encoder + RVQ encode == transformers DacModel.encode (dac_enc.npz)."""
     W, wav, z_ref, codes_ref = load_enc_case()

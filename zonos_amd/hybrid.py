@@ -68,11 +68,15 @@ class HybridEngineConfig:
     def from_backbone_config(cls, bc) -> "HybridEngineConfig":
         """zonos.config.BackboneConfig of a hybrid checkpoint (mamba_ssm create_block arguments)."""
         a, s = dict(bc.attn_cfg or {}), dict(bc.ssm_cfg or {})
-        if s.pop("layer", "Mamba2") != "Mamba2":
+        has_ssm = len(set(bc.attn_layer_idx or [])) < bc.n_layer
+        # mamba_ssm create_block: ssm_cfg.pop("layer", "Mamba1") selects the SSM layer class
+        if has_ssm and s.pop("layer", "Mamba1") != "Mamba2":
             raise ValueError("only Mamba2 SSM layers are supported")
         if a.get("qkv_proj_bias", False) or a.get("out_proj_bias", False):
             raise ValueError("biased attention projections are not supported")
-        if bc.d_intermediate != 0 or bc.rms_norm or bc.residual_in_fp32:
+        if a.get("rotary_emb_interleaved", False):
+            raise ValueError("interleaved rotary embeddings are not supported (GPT-NeoX rotate-half only)")
+        if (has_ssm and bc.d_intermediate != 0) or bc.rms_norm or bc.residual_in_fp32:
             raise ValueError("hybrid variant not supported (d_intermediate / rms_norm / residual_in_fp32)")
         if a.get("rotary_emb_dim", bc.d_model // a.get("num_heads", 16)) != bc.d_model // a.get("num_heads", 16):
             raise ValueError("partial rotary embeddings are not supported")
@@ -92,15 +96,13 @@ def rotary_table(seq_len: int, dim: int, base: float = 10000.0) -> torch.Tensor:
                        dim=-1).contiguous()
 
 
-class HybridDecoder(HipDecoder):
-    """generate() for the hybrid backbone (the layer loop and state differ from HipDecoder)."""
+class HybridBackbone:
+    """The hybrid layers + final LayerNorm on the device (_mamba_ssm.py:9-57): bf16 weights in the
+    engine's layouts and the per-layer launch sequence. Shared by the generate() engine
+    (HybridDecoder) and the backbone plugin (zonos_amd.backbone.HipHybridBackbone); ``prefix`` is
+    "backbone." for a Zonos state dict and "" for the backbone's own."""
 
-    small_batch_path = False      # the hybrid block sequence has its own _layers (prenorm add + norm)
-    # the step / prefill sequences are enqueued by the C ABI (zk_hybrid_decode_step / zk_hybrid_prefill);
-    # False issues the same sequence from Python (bit-identical; the reference for the test)
-    c_step = True
-
-    def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda"):
+    def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda", prefix: str = "backbone."):
         _lib.load()
         if cfg.d_conv != 4 or cfg.ngroups != 1:
             raise ValueError("Mamba2 d_conv=4, ngroups=1 only")
@@ -111,23 +113,15 @@ class HybridDecoder(HipDecoder):
         dev, bf = self.device, torch.bfloat16
 
         def w(name):
-            return weights[name].to(device=dev, dtype=bf).contiguous()
+            return weights[prefix + name].to(device=dev, dtype=bf).contiguous()
 
         def f32(name):
-            return weights[name].to(device=dev, dtype=bf).float().contiguous()
+            return weights[prefix + name].to(device=dev, dtype=bf).float().contiguous()
 
         stream = _lib.stream_ptr(dev)
-        self.emb = torch.stack([w(f"embeddings.{k}.weight") for k in range(N_CB)]).contiguous()
-        heads = []
-        for k in range(N_CB):
-            h = w(f"heads.{k}.weight")
-            if h.shape[0] < VOCAB:
-                h = torch.cat([h, h.new_zeros(VOCAB - h.shape[0], h.shape[1])])
-            heads.append(h)
-        self.heads = pack_weights(torch.cat(heads).contiguous(), stream)
         self.layers = []
         for i in range(cfg.n_layer):
-            p = f"backbone.layers.{i}."
+            p = f"layers.{i}."
             L = dict(ln1_w=w(p + "norm.weight"), ln1_b=w(p + "norm.bias"))
             if i in cfg.attn_layer_idx:
                 fc1 = w(p + "mlp.fc1.weight")
@@ -138,20 +132,117 @@ class HybridDecoder(HipDecoder):
                          ln2_w=w(p + "norm2.weight"), ln2_b=w(p + "norm2.bias"),
                          fc1=pack_weights(fc1p, stream), fc2=pack_weights(w(p + "mlp.fc2.weight"), stream))
             else:
-                cw = weights[p + "mixer.conv1d.weight"].to(device=dev, dtype=bf).float()
+                cw = weights[prefix + p + "mixer.conv1d.weight"].to(device=dev, dtype=bf).float()
                 L.update(type="mamba", w_in=pack_weights(w(p + "mixer.in_proj.weight"), stream),
                          conv_w=cw.reshape(cfg.conv_dim, cfg.d_conv).contiguous(),
                          conv_b=f32(p + "mixer.conv1d.bias"),
-                         A=(-torch.exp(weights[p + "mixer.A_log"].to(bf).float())).to(dev).contiguous(),
+                         A=(-torch.exp(weights[prefix + p + "mixer.A_log"].to(bf).float())).to(dev).contiguous(),
                          dt_bias=f32(p + "mixer.dt_bias"), D=f32(p + "mixer.D"),
                          norm_w=f32(p + "mixer.norm.weight"),
                          w_out=pack_weights(w(p + "mixer.out_proj.weight"), stream))
             self.layers.append(L)
         self.attn_ids = [i for i in range(cfg.n_layer) if i in cfg.attn_layer_idx]
         self.mamba_ids = [i for i in range(cfg.n_layer) if i not in cfg.attn_layer_idx]
-        self.lnf_w = w("backbone.norm_f.weight")
-        self.lnf_b = w("backbone.norm_f.bias")
+        self.lnf_w = w("norm_f.weight")
+        self.lnf_b = w("norm_f.bias")
         self.freqs = rotary_table(16384, cfg.head_dim, cfg.rotary_base).to(dev)
+
+    def _kv(self, ws, layer):
+        if "kv_layers" in ws:            # caches handed out per layer (backbone plugin)
+            kv = ws["kv_layers"][layer]
+            return kv[0], kv[1]
+        j = self.attn_ids.index(layer)
+        return ws["kv"][j, 0], ws["kv"][j, 1]
+
+    def _states(self, ws, layer):
+        """(conv, ssm) state pair of a Mamba layer, each [2 parity buffers][...]."""
+        if "state_layers" in ws:         # backbone plugin
+            return ws["state_layers"][layer]
+        j = self.mamba_ids.index(layer)
+        return ws["conv"][j], ws["ssm"][j]
+
+    # ------------------------------------------------------------------ layer loop
+    def _layers(self, ws, M: int, R: int, S: int, prefill: bool, stream, skip):
+        c = self.cfg
+        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+        di, nin, nh = c.d_inner, c.d_in_proj, c.nheads_ssm
+        Nqkv = (H + 2 * Hk) * hd
+        sp = ws["splits"] if not prefill else dict(qkv=1, o=1, fc2=1, inp=1, out=1)
+        x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
+        scal = ws["scal"]
+        pos_dev = None if prefill else ptr(scal[1:2])
+        for i, L in enumerate(self.layers):
+            if i + 1 < len(self.layers):
+                nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
+            else:
+                nw, nb = self.lnf_w, self.lnf_b
+            if L["type"] == "attn":
+                kc, vt = self._kv(ws, i)
+                call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip,
+                     stream)
+                if prefill:
+                    call("zk_qkv_rope", ptr(part), 1, R, S, H, Hk, hd, ptr(self.freqs), 0, None, ptr(q), ptr(kc),
+                         ptr(vt), ws["smax"], None, 1, skip, stream)
+                    call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
+                else:
+                    call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                         ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), 1, skip,
+                         stream)
+                call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip,
+                     stream)
+                call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D,
+                     ptr(x), ptr(xn), 1, skip, stream)
+                call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fd, D, 1, 1, None, ptr(h), skip, stream)
+                call("zk_gemm_bf16", ptr(h), Fd, ptr(L["fc2"]), M, D, Fd, sp["fc2"], 0, ptr(part), None, skip, stream)
+                call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 1,
+                     skip, stream)
+            else:
+                conv, ssm = self._states(ws, i)
+                # SSM state double-buffered by position parity
+                sr = S & 1
+                ssm_b = ptr(ssm[1])
+                call("zk_gemm_bf16", ptr(xn), D, ptr(L["w_in"]), M, nin, D, sp["inp"], 0, ptr(part), None, skip,
+                     stream)
+                if prefill:
+                    # the first decode step (position S) reads conv buffer (S & 1)
+                    call("zk_mamba_prefill", ptr(part), R, S, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
+                         ptr(L["conv_b"]), ptr(ws["xc"]), ptr(conv[S & 1]), ptr(ssm[sr]), ptr(L["A"]),
+                         ptr(L["dt_bias"]),
+                         ptr(L["D"]), ptr(ws["yz"]), stream)
+                else:
+                    call("zk_mamba_step", ptr(part), sp["inp"], R, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
+                         ptr(L["conv_b"]), ptr(conv[0]), ptr(conv[1]), pos_dev, ptr(ssm[0]), ssm_b, ptr(L["A"]),
+                         ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), skip, stream)
+                call("zk_gated_rmsnorm", ptr(ws["yz"]), M, di, ptr(L["norm_w"]), 1e-5, ptr(ws["ym"]), skip, stream)
+                call("zk_gemm_bf16", ptr(ws["ym"]), di, ptr(L["w_out"]), M, D, di, sp["out"], 0, ptr(part), None,
+                     skip, stream)
+                call("zk_resid_ln", ptr(part), sp["out"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 1,
+                     skip, stream)
+
+
+class HybridDecoder(HybridBackbone, HipDecoder):
+    """generate() for the hybrid backbone (the layer loop and state differ from HipDecoder)."""
+
+    small_batch_path = False      # the hybrid block sequence has its own _layers (prenorm add + norm)
+    # the step / prefill sequences are enqueued by the C ABI (zk_hybrid_decode_step / zk_hybrid_prefill);
+    # False issues the same sequence from Python (bit-identical; the reference for the test)
+    c_step = True
+
+    def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda"):
+        HybridBackbone.__init__(self, cfg, weights, device)
+        dev, bf = self.device, torch.bfloat16
+
+        def w(name):
+            return weights[name].to(device=dev, dtype=bf).contiguous()
+
+        self.emb = torch.stack([w(f"embeddings.{k}.weight") for k in range(N_CB)]).contiguous()
+        heads = []
+        for k in range(N_CB):
+            h = w(f"heads.{k}.weight")
+            if h.shape[0] < VOCAB:
+                h = torch.cat([h, h.new_zeros(VOCAB - h.shape[0], h.shape[1])])
+            heads.append(h)
+        self.heads = pack_weights(torch.cat(heads).contiguous(), _lib.stream_ptr(dev))
         self._ws = None
         torch.cuda.synchronize(dev)
 
@@ -212,10 +303,6 @@ class HybridDecoder(HipDecoder):
         self._ws = ws
         return ws
 
-    def _kv(self, ws, layer):
-        j = self.attn_ids.index(layer)
-        return ws["kv"][j, 0], ws["kv"][j, 1]
-
     # ------------------------------------------------------------------ C ABI descriptor
     def _step_desc(self, ws, B, st, sp):
         """zk_hybrid_desc of this workspace: per-layer weights + states, buffers, state, params."""
@@ -255,61 +342,3 @@ class HybridDecoder(HipDecoder):
     def _c_prefill(self, ws, B, st, sp, cond, Lc, P, stream):
         call("zk_hybrid_prefill", C.byref(self._step_desc(ws, B, st, sp)), ptr(cond), Lc, P, ptr(ws["q"]), stream)
 
-    # ------------------------------------------------------------------ layer loop
-    def _layers(self, ws, M: int, R: int, S: int, prefill: bool, stream, skip):
-        c = self.cfg
-        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
-        di, nin, nh = c.d_inner, c.d_in_proj, c.nheads_ssm
-        Nqkv = (H + 2 * Hk) * hd
-        sp = ws["splits"] if not prefill else dict(qkv=1, o=1, fc2=1, inp=1, out=1)
-        x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
-        scal = ws["scal"]
-        pos_dev = None if prefill else ptr(scal[1:2])
-        for i, L in enumerate(self.layers):
-            if i + 1 < len(self.layers):
-                nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
-            else:
-                nw, nb = self.lnf_w, self.lnf_b
-            if L["type"] == "attn":
-                kc, vt = self._kv(ws, i)
-                call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip,
-                     stream)
-                if prefill:
-                    call("zk_qkv_rope", ptr(part), 1, R, S, H, Hk, hd, ptr(self.freqs), 0, None, ptr(q), ptr(kc),
-                         ptr(vt), ws["smax"], None, 1, skip, stream)
-                    call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
-                else:
-                    call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
-                         ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), 1, skip,
-                         stream)
-                call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip,
-                     stream)
-                call("zk_resid_ln", ptr(part), sp["o"], ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D,
-                     ptr(x), ptr(xn), 1, skip, stream)
-                call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fd, D, 1, 1, None, ptr(h), skip, stream)
-                call("zk_gemm_bf16", ptr(h), Fd, ptr(L["fc2"]), M, D, Fd, sp["fc2"], 0, ptr(part), None, skip, stream)
-                call("zk_resid_ln", ptr(part), sp["fc2"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 1,
-                     skip, stream)
-            else:
-                j = self.mamba_ids.index(i)
-                conv, ssm = ws["conv"][j], ws["ssm"][j]
-                # SSM state double-buffered by position parity
-                sr = S & 1
-                ssm_b = ptr(ssm[1])
-                call("zk_gemm_bf16", ptr(xn), D, ptr(L["w_in"]), M, nin, D, sp["inp"], 0, ptr(part), None, skip,
-                     stream)
-                if prefill:
-                    # the first decode step (position S) reads conv buffer (S & 1)
-                    call("zk_mamba_prefill", ptr(part), R, S, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
-                         ptr(L["conv_b"]), ptr(ws["xc"]), ptr(conv[S & 1]), ptr(ssm[sr]), ptr(L["A"]),
-                         ptr(L["dt_bias"]),
-                         ptr(L["D"]), ptr(ws["yz"]), stream)
-                else:
-                    call("zk_mamba_step", ptr(part), sp["inp"], R, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
-                         ptr(L["conv_b"]), ptr(conv[0]), ptr(conv[1]), pos_dev, ptr(ssm[0]), ssm_b, ptr(L["A"]),
-                         ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), skip, stream)
-                call("zk_gated_rmsnorm", ptr(ws["yz"]), M, di, ptr(L["norm_w"]), 1e-5, ptr(ws["ym"]), skip, stream)
-                call("zk_gemm_bf16", ptr(ws["ym"]), di, ptr(L["w_out"]), M, D, di, sp["out"], 0, ptr(part), None,
-                     skip, stream)
-                call("zk_resid_ln", ptr(part), sp["out"], ptr(x), ptr(nw), ptr(nb), c.eps, M, D, ptr(x), ptr(xn), 1,
-                     skip, stream)

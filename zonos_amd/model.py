@@ -66,14 +66,30 @@ class Zonos:
     @classmethod
     def from_local(cls, config_path: str, model_path: str, device=DEFAULT_DEVICE, backbone: str | None = None,
                    autoencoder: DACAutoencoder | None = None) -> "Zonos":
+        """model.py:65-88. ``backbone`` selects a class of the registry (zonos_amd.backbone.BACKBONES,
+        the reference's keys included) exactly as the reference does: an unknown name raises KeyError,
+        and a class whose ``supported_architectures`` lacks the checkpoint's architecture raises
+        ValueError (the reference's torch backbone asserts on a hybrid config, _torch.py:56). The
+        selected plugin runs the same kernels as the engine, so generate() is unchanged by it."""
         from safetensors import safe_open
+
+        from .backbone import BACKBONES
         config = ZonosConfig.from_dict(json.load(open(config_path)))
+        if backbone:
+            bcls = BACKBONES[backbone]
+            arch = "hybrid" if is_hybrid(config.backbone) else "transformer"
+            if arch not in bcls.supported_architectures:
+                raise ValueError(f"backbone {backbone!r} ({bcls.__name__}) does not support the {arch} "
+                                 f"architecture (supported: {bcls.supported_architectures})")
         sd = {}
         with safe_open(model_path, framework="pt") as f:
             for k in f.keys():
                 if k.startswith(("backbone.", "embeddings.", "heads.", "prefix_conditioner.")):
                     sd[k] = f.get_tensor(k)
-        return cls(config, sd, device, autoencoder)
+        model = cls(config, sd, device, autoencoder)
+        if backbone:
+            model.backbone_name = backbone
+        return model
 
     def prepare_conditioning(self, cond_dict: dict, uncond_dict: dict | None = None) -> torch.Tensor:
         """model.py:210-218: [2B, L, d_model] bf16 = cat(PrefixConditioner(cond), PrefixConditioner(uncond))."""
