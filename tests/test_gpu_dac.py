@@ -150,14 +150,17 @@ def _tiles_per_workgroup(B, Qn, Cout, resid=False, nphase=1):
 
 
 def test_dac_long_golden_multitile():
-    """The c3 regime: every decoder stage after the first streams >= 2 tiles per persistent
-    workgroup (tile carry-over of the loader rings, dac_cl.hip:148-160). fp16 decode of 2 x 600
-    frames vs the reference DacModel: RMS <= 1e-4 (north_star), both rows."""
+    """The c3 regime: the 384-, 192- and 96-channel stages (k7 in the fat 12-wave form and in the
+    two-per-CU form, the residual 1x1 convs, the ConvTranspose into them) stream >= 2 tiles per
+    persistent workgroup (tile carry-over of the loader rings, dac_cl.hip:148-160). fp16 decode of
+    2 x 600 frames vs the reference DacModel: RMS <= 1e-4 (north_star), both rows. (The 1536- and
+    768-channel stages stay below the resident count at this length; their multi-tile forms are
+    test_gpu_dac_cl.py's MULTITILE_CASES.)"""
     dec, d, codes, wav, _ = _long()
-    # the stages' (rows, positions, channels): 8x at 768 ch, 64x at 384 (x4 tiles), 512x at 96
+    # the stages' (rows, positions, channels): 64x at 384, 256x at 192, 512x at 96
     T = codes.shape[2]
-    assert _tiles_per_workgroup(2, 8 * T, 768, resid=True) >= 2
-    assert _tiles_per_workgroup(2, 64 * T, 384) >= 2
+    assert _tiles_per_workgroup(2, 64 * T, 384) >= 2 and _tiles_per_workgroup(2, 64 * T, 384, resid=True) >= 2
+    assert _tiles_per_workgroup(2, 256 * T, 192) >= 2 and _tiles_per_workgroup(2, 256 * T, 192, resid=True) >= 2
     assert _tiles_per_workgroup(2, 512 * T, 96) >= 2 and _tiles_per_workgroup(2, 512 * T, 96, resid=True) >= 2
     got = dec.decode_padded(codes).cpu()
     assert got.shape == wav.shape

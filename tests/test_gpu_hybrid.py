@@ -381,18 +381,24 @@ def test_hybrid_backbone_plugin_matches_oracle():
     print("hybrid plugin vs oracle |d| (max, mean) per call:", errs)
     # LayerNorm'd outputs (|x| ~ 1): bf16 ulps plus the SSM state's bf16 rounding
     assert max(e[0] for e in errs) < 0.15 and max(e[1] for e in errs) < 0.015, errs
-    # the Mamba states the plugin advanced equal the restatement's (SSM within bf16 rounding)
+    # the Mamba states the plugin advanced equal the restatement's within bf16 rounding: the conv
+    # state holds in_proj outputs (bf16), whose GEMM reduction order differs from the CPU's
     for i in (0, 1, 3):
         conv, ssm = ip.key_value_memory_dict[i]
         par = (S + n_dec) & 1                                # parity buffer the next step reads
-        assert torch.equal(conv[par].cpu(), cache.conv[i])
+        dc = (conv[par].float().cpu() - cache.conv[i].float()).abs()
+        # (the in_proj input differs by the upstream layers' bf16 ulps as well: measured max 0.016)
+        assert dc.max() <= 0.05 and dc.mean() <= 2e-3, (float(dc.max()), float(dc.mean()))
         d = (ssm[par].float().cpu() - cache.ssm[i].float()).abs()
         assert d.max() <= 2 ** -6 * cache.ssm[i].float().abs().max(), float(d.max())
 
 
-# c5 long-run bounds, from the measured error growth on MI355X (see the test's print): fp32 CFG logits
-# of the engine (decode-step graph at B = 64, 2570 teacher-forced steps) vs the restatement
-C5_MAX, C5_MEAN = 1.5, 0.15
+# c5 long-run bounds from the measured error growth on MI355X (profiles/r4_hybrid_c5_long_test.txt):
+# fp32 CFG logits of the engine (decode-step graph at B = 64, 2570 teacher-forced steps) vs the
+# restatement, max 0.22-0.28 / mean 0.043-0.046 at every recorded step from 0 to 2570 -- flat, no drift
+# of the recurrent bf16 SSM states. Bounds = 1.4x the measured worst step; the late steps' mean error
+# may not exceed the first steps' by more than 25 %.
+C5_MAX, C5_MEAN, C5_DRIFT = 0.4, 0.065, 1.25
 
 
 def test_hybrid_c5_workload_teacher_forced_long():
@@ -443,7 +449,9 @@ def test_hybrid_c5_workload_teacher_forced_long():
     ref = d["logits"].astype(np.float32)                        # [U][steps][9][V]
     rows = []
     for j, s in enumerate(want):
-        r, g = ref[:, j], got[s]
+        r, g = ref[:, j].copy(), got[s].copy()
+        if s == 0:       # the restatement records step 0 after benchmark mode's EOS mask (zonos_ref.generate)
+            r[:, 0, 1024] = g[:, 0, 1024] = -np.inf
         fin = np.isfinite(r)
         assert np.array_equal(fin, np.isfinite(g))
         e = np.abs(g[fin] - r[fin])
@@ -456,3 +464,6 @@ def test_hybrid_c5_workload_teacher_forced_long():
         assert np.array_equal(rr.argmax(-1)[ok], gg.argmax(-1)[ok]), s
     print("hybrid c5 (step, max |d|, mean |d|, mean |logit|):", rows)
     assert max(r[1] for r in rows) < C5_MAX and max(r[2] for r in rows) < C5_MEAN, rows
+    early = np.mean([r[2] for r in rows if r[0] < 3])
+    late = np.mean([r[2] for r in rows if r[0] > 2500])
+    assert late <= C5_DRIFT * early, (early, late)

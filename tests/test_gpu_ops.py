@@ -81,7 +81,10 @@ def test_delay_pattern_golden():
                                           (128, 2048, 2048, 8), (128, 9234, 2048, 2), (128, 16384, 2048, 1),
                                           (128, 2048, 2048, 4), (100, 2048, 8192, 4), (1, 3072, 2048, 2),
                                           # prefill shapes (k_gemm, M >= 1024)
-                                          (1100, 256, 512, 1), (2048, 384, 2048, 1), (1024, 1152, 128, 1)])
+                                          (1100, 256, 512, 1), (2048, 384, 2048, 1), (1024, 1152, 128, 1),
+                                          # prefill shapes with >= 256 tiles of 256 x 256 (k_gemm_pf): ragged
+                                          # last row block, N not a multiple of 256 (hybrid in_proj), K = 8192
+                                          (16400, 4096, 1024, 1), (8300, 8512, 512, 1), (9000, 2048, 8192, 1)])
 def test_gemm_vs_fp32(M, N, K, nsplit):
     from zonos_amd._lib import call, ptr, stream_ptr
     g = torch.Generator(device="cpu").manual_seed(M + N)
@@ -115,13 +118,16 @@ def test_pack_weights_layout():
 
 
 @pytest.mark.parametrize("M,Fd,D", [(130, 256, 512), (2, 256, 512), (40, 256, 512), (128, 512, 2048),
-                                    (3, 512, 2048), (1030, 256, 512)])
+                                    (3, 512, 2048), (1030, 256, 512), (8200, 4096, 1024)])
 def test_gemm_swiglu(M, Fd, D):
     from zonos_amd._lib import call, ptr, stream_ptr
     g = torch.Generator(device="cpu").manual_seed(1)
     A = torch.randn(M, D, generator=g).to(torch.bfloat16)
     W1 = (torch.randn(2 * Fd, D, generator=g) / D ** 0.5).to(torch.bfloat16)
-    ref_y, ref_g = F.linear(A, W1).chunk(2, dim=-1)      # bf16 CPU like the reference
+    if M * Fd * D < 2 ** 30:
+        ref_y, ref_g = F.linear(A, W1).chunk(2, dim=-1)      # bf16 CPU like the reference
+    else:                                                     # (the k_gemm_pf size: fp32 GEMM on the GPU, bf16-rounded)
+        ref_y, ref_g = (A.to(DEV).float() @ W1.to(DEV).float().t()).bfloat16().cpu().chunk(2, dim=-1)
     ref = ref_y * F.silu(ref_g)
     Wp = torch.empty_like(W1).to(DEV)
     s = stream_ptr()

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libzonos_hip.so")
-SOURCES = ["sampler.hip", "backbone.hip", "gemm.hip", "dac.hip", "dac_mfma.hip", "dac_cl.hip", "post.hip", "mamba.hip", "cond.hip", "capi.cpp"]
+SOURCES = ["sampler.hip", "backbone.hip", "gemm.hip", "gemm_pf.hip", "dac.hip", "dac_mfma.hip", "dac_cl.hip", "post.hip", "mamba.hip", "cond.hip", "capi.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ZK_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no implicit FMA contraction -- the reference rounds every elementwise op

@@ -129,8 +129,8 @@ extern "C" int zk_event_destroy(void* ev) {
 #ifndef ZK_L2_WARM
 #define ZK_L2_WARM 1
 #endif
-static ZkWarm warm_desc(const void* W, int M, int N, int K, int nsplit) {
-    return ZK_L2_WARM ? zk_gemm_warm_desc(W, M, N, K, nsplit, 2) : ZkWarm{nullptr, 0, 0, 0, 0};
+static ZkWarm warm_desc(const void* W, int M, int N, int K, int nsplit, int mode = 0) {
+    return ZK_L2_WARM ? zk_gemm_warm_desc(W, M, N, K, nsplit, mode, 2) : ZkWarm{nullptr, 0, 0, 0, 0};
 }
 
 extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
@@ -178,7 +178,7 @@ extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
             ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, R, D, H * hd, d->split_o, 0, d->part, nullptr, skip, stream));
             // each k_resid_ln and the fc1 GEMM warm the next GEMM's first weight chunks into L2 (warm.h)
             ZK_STEP(zk_resid_ln_warm(d->part, d->split_o, d->x, L.ln2_w, L.ln2_b, d->eps, R, D, d->x, d->xn, 0, skip,
-                                     warm_desc(L.fc1, R, 2 * Fd, D, 1), stream));
+                                     warm_desc(L.fc1, R, 2 * Fd, D, 1, 1), stream));
             ZK_STEP(zk_gemm_bf16_warm(d->xn, D, L.fc1, R, 2 * Fd, D, 1, 1, nullptr, d->h, skip,
                                       warm_desc(L.fc2, R, D, Fd, d->split_fc2), stream));
             ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, R, D, Fd, d->split_fc2, 0, d->part, nullptr, skip, stream));
@@ -298,7 +298,7 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
             }
             ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, M, D, H * hd, so, 0, d->part, nullptr, skip, stream));
             ZK_STEP(zk_resid_ln_warm(d->part, so, d->x, L.ln2_w, L.ln2_b, d->eps, M, D, d->x, d->xn, 1, skip,
-                                     prefill ? ZkWarm{nullptr, 0, 0, 0, 0} : warm_desc(L.fc1, M, 2 * Fd, D, 1), stream));
+                                     prefill ? ZkWarm{nullptr, 0, 0, 0, 0} : warm_desc(L.fc1, M, 2 * Fd, D, 1, 1), stream));
             ZK_STEP(zk_gemm_bf16_warm(d->xn, D, L.fc1, M, 2 * Fd, D, 1, 1, nullptr, d->h, skip,
                                       prefill ? ZkWarm{nullptr, 0, 0, 0, 0} : warm_desc(L.fc2, M, D, Fd, sf), stream));
             ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, M, D, Fd, sf, 0, d->part, nullptr, skip, stream));

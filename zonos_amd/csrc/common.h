@@ -85,16 +85,21 @@ ZK_DEV void ws_tile(int L, int gx, int gz, int& bx, int& bz) {
 // 2 KB). Issue them as LDS-DMA (default cache policy, so the lines stay in this XCD's L2) into a
 // 1 KB LDS sink the issuing wave never reads: no registers, nothing for the other waves to wait on.
 // Returns the number of loads issued (2 per chunk).
+// `chunks` packs the GEMM's column groups per compute wave (k_gemm_ws NG) in bits 8+: wave w of
+// workgroup (bx, bz) streams the 16-row tiles (bx * 4 + w) * NG + g, g < NG.
 ZK_DEV int warm_unit(const bf16_t* W, int K, int gx, int gz, int chunks, int L, int w, int lane, void* sink) {
     int bx, bz;
     ws_tile(L, gx, gz, bx, bz);
+    const int ng = max(1, chunks >> 8), nch = chunks & 255;
     const int kbeg = bz * (K / gz);
-    const bf16_t* p = W + ((size_t)(bx * 4 + w) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
-    for (int c = 0; c < chunks; ++c) {
-        __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024), sink, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024 + 512), sink, 16, 0, 0);
+    for (int g = 0; g < ng; ++g) {
+        const bf16_t* p = W + ((size_t)((bx * 4 + w) * ng + g) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
+        for (int c = 0; c < nch; ++c) {
+            __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024), sink, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024 + 512), sink, 16, 0, 0);
+        }
     }
-    return 2 * chunks;
+    return 2 * nch * ng;
 }
 
 // All warm-up units of workgroup r of an nwg-workgroup launch (nwg % 8 == 0 keeps the GEMM

@@ -270,7 +270,12 @@ ZK_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory")
 
 // MT = 16-row M tiles actually present (1, 2, 4, 8): small batches stage and multiply only
 // the rows they have (B = 1 decode: 2 rows -> one 16-row tile instead of 8).
-template <int MODE, int NCH, int PF, int MT, int NCW = 4>
+// NG = 16-column groups per compute wave: every activation fragment read from LDS feeds NG MFMAs,
+// and a workgroup covers 16 * NCW * NG columns, so a wider tile stages the same activation once
+// for NG times the weights (LDS reads and per-CU activation intake per weight byte / NG).
+// NB = activation fragment buffers (2: the next chunk's fragments are read while this one is
+// multiplied).
+template <int MODE, int NCH, int PF, int MT, int NCW = 4, int NG = 1, int NB = (NCW > 4 ? 1 : 2)>
 __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
     if (skip && *skip) return;
     int bx, bz;
     ws_tile(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x, gridDim.z, bx, bz);     // gridDim.y == 1
-    constexpr int BNW = 16 * NCW;                 // columns per workgroup (16 per compute wave)
+    constexpr int BNW = 16 * NCW * NG;            // columns per workgroup
     const int n0 = bx * BNW, split = bz;
     const int kbeg = split * kslice;
     const int nchunks = kslice / BK;
@@ -347,30 +352,37 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
         return;
     }
 
-    // ---------------- compute waves
-    const int wn = n0 + w * 16 + ln;
-    const bool wvalid = wn < N;
-    // a 16-row tile wholly past N streams tile 0 (never stored): the packed image ends at ceil64(N)
-    const int trow = n0 + w * 16 < N ? n0 + w * 16 : 0;
-    const bf16_t* wrow = w_base(W, trow, wvalid ? wn : 0, K, kbeg, lane);
-    f32x4 acc[MT];
+    // ---------------- compute waves: wave w owns the 16-column groups w * NG + g
+    const bf16_t* wrow[NG];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < NG; ++g) {
+        const int c0 = n0 + (w * NG + g) * 16;
+        // a 16-row tile wholly past N streams tile 0 (never stored): the packed image ends at ceil64(N)
+        const int trow = c0 < N ? c0 : 0;
+        wrow[g] = w_base(W, trow, c0 + ln < N ? c0 + ln : 0, K, kbeg, lane);
+    }
+    f32x4 acc[NG][MT];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[g][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     // Fully unrolled K loop (NCH chunks known at compile time): no loop back edge, so hipcc's
-    // waitcnt pass counts exactly and keeps PF chunks (2 loads each) of weights in flight
+    // waitcnt pass counts exactly and keeps PF chunks (2 loads per group each) of weights in flight
     // (its loop-header merge otherwise drains the ring). Ring slots are compile-time indices.
     constexpr int U = PF + 1;
-    uint4 wr0[U], wr1[U];
+    uint4 wr0[NG][U], wr1[NG][U];
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
         const int pc = p < NCH ? p : NCH - 1;
-        wr0[p] = ldg_w<WS_NT>(wrow + pc * WCH);
-        wr1[p] = ldg_w<WS_NT>(wrow + pc * WCH + WHALF);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            wr0[g][p] = ldg_w<WS_NT>(wrow[g] + pc * WCH);
+            wr1[g][p] = ldg_w<WS_NT>(wrow[g] + pc * WCH + WHALF);
+        }
     }
     // activation fragments of the next chunk are read from LDS (register double buffer) while
     // the current chunk is multiplied: the LDS latency after each barrier is off the MFMA path
-    // (NCW > 4: 3 waves per SIMD leave 168 VGPRs -- one fragment set, read after the MFMAs)
-    constexpr int NB = NCW > 4 ? 1 : 2;
+    // (NB = 1: one fragment set, read after the MFMAs)
     uint4 af[NB][2][MT];
     auto read_frags = [&](int ch, int buf) {
         const char* base = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
@@ -386,8 +398,11 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
         if (ch + PF < NCH) {
-            wr0[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH);
-            wr1[(ch + PF) % U] = ldg_w<WS_NT>(wrow + (ch + PF) * WCH + WHALF);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                wr0[g][(ch + PF) % U] = ldg_w<WS_NT>(wrow[g] + (ch + PF) * WCH);
+                wr1[g][(ch + PF) % U] = ldg_w<WS_NT>(wrow[g] + (ch + PF) * WCH + WHALF);
+            }
         }
         if (NB == 2 && ch + 1 < NCH) {
             __builtin_amdgcn_s_barrier();                           // chunk ch+1 (and ch+2) in LDS
@@ -397,11 +412,14 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
         __builtin_amdgcn_sched_barrier(0);     // keep the fragment reads ahead of this chunk's MFMAs
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const bf16x8 b = as_frag(ks == 0 ? wr0[ch % U] : wr1[ch % U]);
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(af[NB == 2 ? (ch & 1) : 0][ks][mt]), b,
-                                                                  acc[mt], 0, 0, 0);
+            for (int mt = 0; mt < MT; ++mt) {
+                const bf16x8 a = as_frag(af[NB == 2 ? (ch & 1) : 0][ks][mt]);
+#pragma unroll
+                for (int g = 0; g < NG; ++g)
+                    acc[g][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        a, as_frag(ks == 0 ? wr0[g][ch % U] : wr1[g][ch % U]), acc[g][mt], 0, 0, 0);
+            }
         }
         if (NB == 1 && ch + 1 < NCH) {
             __builtin_amdgcn_sched_barrier(0);
@@ -412,34 +430,32 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
     }
     if (ZK_WS_EPI && (MODE == 1 || N % 4 == 0)) {
         // Epilogue staged through the (now idle) LDS ring so that every store instruction writes
-        // whole rows: slabs 4 rows x 256 B (full 128-B lines) per instruction instead of 4 x 64-B
-        // pieces, SwiGLU 16 rows x 64 B instead of 16-B pieces. (The loader waves have exited; a
-        // workgroup barrier no longer counts them.)
+        // whole rows: slabs of BNW floats per row (full 128-B lines) instead of 64-B pieces, SwiGLU
+        // rows of BNW / 2 bf16 instead of 16-B pieces. (The loader waves have exited; a workgroup
+        // barrier no longer counts them.)
         constexpr int TS = BNW + 4;                              // fp32 tile row stride (+ pad)
         float* tile = reinterpret_cast<float*>(smem);
         __syncthreads();                                         // every wave's last LDS fragment read
-        if (MODE == 0) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) tile[(mt * 16 + lg * 4 + i) * TS + w * 16 + ln] = acc[mt][i];
-        } else {
-            // the bf16-rounded y / gate columns as they are (8 + 8 interleaved per 16-column group);
-            // SwiGLU runs in the store pass below, on every lane (here it would run on half the lanes
-            // behind a branch per value: fc1 23.4 -> 18.x us)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) tile[(mt * 16 + lg * 4 + i) * TS + w * 16 + ln] = round_bf(acc[mt][i]);
-        }
+                for (int i = 0; i < 4; ++i)
+                    // MODE 1: the bf16-rounded y / gate columns as they are (8 + 8 interleaved per
+                    // 16-column group); SwiGLU runs in the store pass below, on every lane (here it
+                    // would run on half the lanes behind a branch per value: fc1 23.4 -> 18.x us)
+                    tile[(mt * 16 + lg * 4 + i) * TS + (w * NG + g) * 16 + ln] =
+                        MODE == 0 ? acc[g][mt][i] : round_bf(acc[g][mt][i]);
         __syncthreads();
         if (MODE == 0) {
             float* C = Cpart + (size_t)split * M * N;
-            constexpr int LPR = 4 * NCW;                         // lanes per row (4 floats each)
+            constexpr int LPR = BNW / 4;                         // lanes per row (4 floats each)
+            constexpr int RPI = 64 / LPR;                        // whole rows per instruction
             const int c4 = (lane % LPR) * 4;
 #pragma unroll
-            for (int q = w; q < MT * NCW; q += NCW) {           // 64 / LPR whole rows per instruction
-                const int m = q * (64 / LPR) + lane / LPR;
+            for (int q = w; q < MT * 16 / RPI; q += NCW) {
+                const int m = q * RPI + lane / LPR;
                 if (m < M && n0 + c4 < N) {
                     const f32x4 v = *reinterpret_cast<const f32x4*>(tile + m * TS + c4);
                     float* dst = C + (size_t)m * N + n0 + c4;
@@ -455,10 +471,12 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
             }
         } else {
             const int F = N / 2;
-            const int f0 = n0 / 2, gi = lane % NCW;             // 16-column group gi -> outputs f0 + 8 gi ..
+            constexpr int GPR = BNW / 16;                        // 16-column groups per row
+            constexpr int RPI = 64 / GPR;                        // rows per instruction
+            const int f0 = n0 / 2, gi = lane % GPR;              // group gi -> outputs f0 + 8 gi ..
 #pragma unroll
-            for (int q = w; q < MT * NCW / 4; q += NCW) {        // 64 / NCW rows x 16*NCW B per instruction
-                const int m = q * (64 / NCW) + lane / NCW;
+            for (int q = w; q < MT * 16 / RPI; q += NCW) {
+                const int m = q * RPI + lane / GPR;
                 if (m < M && f0 + gi * 8 < F) {
                     const float* yv = tile + m * TS + gi * 16;
                     float o[8];
@@ -474,32 +492,36 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
         }
         return;
     }
-    if (MODE == 0) {
-        float* C = Cpart + (size_t)split * M * N;
-        if (wvalid) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int wn = n0 + (w * NG + g) * 16 + ln;
+        if (MODE == 0) {
+            float* C = Cpart + (size_t)split * M * N;
+            if (wn < N) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = mt * 16 + lg * 4 + i;
+                        if (m < M) st_slab(C + (size_t)m * N + wn, acc[g][mt][i]);
+                    }
+            }
+        } else {
+            const int F = N / 2;
+            const int f = (n0 + (w * NG + g) * 16) / 2 + (ln & 7);
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
+                    const float mine = round_bf(acc[g][mt][i]);
+                    const float other = __shfl_xor(mine, 8, 64);
                     const int m = mt * 16 + lg * 4 + i;
-                    if (m < M) st_slab(C + (size_t)m * N + wn, acc[mt][i]);
+                    if (ln < 8 && m < M && f < F) {
+                        const float sl = round_bf(other / (1.0f + expf(-other)));
+                        Cout[(size_t)m * F + f] = f2bf(mine * sl);
+                    }
                 }
         }
-    } else {
-        const int F = N / 2;
-        const int f = (n0 + w * 16) / 2 + (ln & 7);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float mine = round_bf(acc[mt][i]);
-                const float other = __shfl_xor(mine, 8, 64);
-                const int m = mt * 16 + lg * 4 + i;
-                if (ln < 8 && m < M && f < F) {
-                    const float sl = round_bf(other / (1.0f + expf(-other)));
-                    Cout[(size_t)m * F + f] = f2bf(mine * sl);
-                }
-            }
     }
 }
 
@@ -953,10 +975,34 @@ static bool ws_regime(int M, int K, int nsplit) {
     return M <= BM && K / nsplit / BK <= 32;
 }
 
-ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int chunks) {
+// k_gemm_ws column groups per compute wave (NG): 16 * 4 * NG columns per workgroup. The slab
+// epilogue needs N % 4 == 0 for its whole-row stores (the heads GEMM, N = 9234, keeps NG = 1).
+#ifndef ZK_WS_NG0
+#define ZK_WS_NG0 1                // split-K slab GEMMs (mode 0)
+#endif
+#ifndef ZK_WS_NG1
+#define ZK_WS_NG1 1                // SwiGLU fc1 (mode 1)
+#endif
+#ifndef ZK_WS_NGNB
+#define ZK_WS_NGNB 1               // activation fragment buffers at NG = 2 (2 exceeds 256 VGPRs at PF 3)
+#endif
+static int ws_ng(int N, int mode) {
+    if (mode == 1) return ZK_WS_NG1;
+    return N % 4 == 0 ? ZK_WS_NG0 : 1;
+}
+
+#ifndef ZK_GEMM_PF
+#define ZK_GEMM_PF 1               // 256 x 256-tile prefill GEMM (gemm_pf.hip) where it fills the chip
+#endif
+bool zk_gemm_pf_applies(int M, int N, int K, int nsplit);
+int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int mode, float* C, void* Cb,
+               const int32_t* skip, void* stream);
+
+ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int mode, int chunks) {
     if (W == nullptr || M <= 16 || ZK_WS_NCW != 4 || !ws_regime(M, K, nsplit) || K % (nsplit * BK) != 0)
         return ZkWarm{nullptr, 0, 0, 0, 0};
-    return ZkWarm{W, K, (N + BN - 1) / BN, nsplit, std::min(chunks, K / nsplit / BK)};
+    const int ng = ws_ng(N, mode);
+    return ZkWarm{W, K, (N + BN * ng - 1) / (BN * ng), nsplit, std::min(chunks, K / nsplit / BK) | (ng > 1 ? ng << 8 : 0)};
 }
 
 extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
@@ -1009,20 +1055,27 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
         }
     }
     if (M <= BM && nchunks <= 32) {
-        constexpr int NCW = ZK_WS_NCW;            // compute waves = 16-column tiles per workgroup
-        dim3 g((N + 16 * NCW - 1) / (16 * NCW), 1, nsplit);
+        constexpr int NCW = ZK_WS_NCW;            // compute waves per workgroup
+        const int ng = M > 16 && NCW == 4 ? ws_ng(N, mode) : 1;
+        dim3 g((N + 16 * NCW * ng - 1) / (16 * NCW * ng), 1, nsplit);
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
         const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2 + (warm.W ? 1024 : 0);     // + warm-up sink
-#define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
+#define ZK_WS_LAUNCH4(MODE_, NCH_, MT_, NG_)                                                                       \
     do {                                                                                                          \
+        constexpr int NB_ = NG_ > 1 ? ZK_WS_NGNB : (NCW > 4 ? 1 : 2);                                             \
+        auto kern_ = &k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW, NG_, NB_>;                        \
         if (lds > 65536)                                                                                          \
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW>),          \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                            \
-        hipLaunchKernelGGL((k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW>), g, dim3(64 * (NCW + WS_NLD)), lds,          \
-                           (hipStream_t)stream,                                                                   \
+            hipFuncSetAttribute(reinterpret_cast<const void*>(kern_), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)lds);                                                                        \
+        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW + WS_NLD)), lds, (hipStream_t)stream,                         \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
                            skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks);              \
         handled = true;                                                                                           \
+    } while (0)
+#define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
+    do {                                                                                                          \
+        if ((MT_) == 8 && ng == 2) ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 2);                                            \
+        else ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 1);                                                                  \
     } while (0)
 #define ZK_WS_LAUNCH(MODE_, NCH_)                                                                                  \
     do {                                                                                                          \
@@ -1056,9 +1109,13 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
             ZK_CHECK_LAUNCH("zk_gemm_bf16");
             return 0;
         }
+#undef ZK_WS_LAUNCH4
 #undef ZK_WS_LAUNCH3
 #undef ZK_WS_LAUNCH
     }
+    // large M (prefill) with at least one 256 x 256 tile per CU: gemm_pf.hip
+    if (ZK_GEMM_PF && zk_gemm_pf_applies(M, N, K, nsplit))
+        return zk_gemm_pf(A, lda, W, M, N, K, mode, Cpart, Cout, skip_flag, stream);
     // large M (prefill): two 16-column tiles per wave for the slab GEMMs (c3 prefill: in_proj
     // 1.01 vs 1.09 ms, fc2 1.98 vs 2.29 ms; the SwiGLU fc1 is faster with one: 4.87 vs 5.24 ms)
     const int ntw = (mode == 0 && M > BM && N >= 8 * BN) ? 2 : 1;

@@ -13,11 +13,11 @@ struct ZkWarm {
     const void* W;     // packed weights of the GEMM to warm (nullptr: off)
     int K;             // GEMM K
     int gx, gz;        // its k_gemm_ws grid (column tiles, K splits)
-    int chunks;        // 64-deep chunks per compute wave to warm
+    int chunks;        // 64-deep chunks per compute wave to warm | column groups per wave (NG) << 8
 };
 
-// k_gemm_ws grid of zk_gemm_bf16(M, N, K, nsplit) in the decode regime, or W = nullptr
-ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int chunks);
+// k_gemm_ws grid of zk_gemm_bf16(M, N, K, nsplit, mode) in the decode regime, or W = nullptr
+ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int mode, int chunks);
 
 int zk_resid_ln_warm(const float* part, int nsplit, const void* x_in, const void* w, const void* b, float eps,
                      int rows, int D, void* x_out, void* xn_out, int ln_on_sum, const int32_t* skip, ZkWarm warm,
