@@ -57,7 +57,7 @@ STUB(zk_dac_tail_cl, const float*, int, int, int, const float*, const float*, fl
 // replaces, so the per-layer launch counts below are the same with and without the L2 warm-up
 #include "../../zonos_amd/csrc/warm.h"
 static int g_warm = 0;              // launches that carried a warm-up descriptor
-ZkWarm zk_gemm_warm_desc(const void* W, int, int N, int K, int nsplit, int chunks) {
+ZkWarm zk_gemm_warm_desc(const void* W, int, int N, int K, int nsplit, int, int chunks) {
     return ZkWarm{W, K, N / 64, nsplit, chunks};
 }
 int zk_resid_ln_warm(const float*, int, const void*, const void*, const void*, float, int, int, void*, void*, int,
