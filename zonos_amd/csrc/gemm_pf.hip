@@ -23,13 +23,16 @@
 
 namespace {
 
-constexpr int PF_BM = 256, PF_BN = 256, PF_BK = 64, PF_NT = 512;
-constexpr int PF_AST = PF_BM * PF_BK * 2;          // activation stage bytes (32 KB)
-constexpr int PF_BST = PF_BN * PF_BK * 2;          // weight stage bytes (32 KB)
-constexpr int PF_ST = PF_AST + PF_BST;             // one stage
-constexpr int PF_LDS = 2 * PF_ST;                  // two stages: 128 KB
+constexpr int PF_BM = 256, PF_BN = 256, PF_NT = 512;
 
-ZK_DEV int pf_lds_off(int row, int c) { return row * 128 + ((c ^ (row & 7)) << 4); }
+// Activation rows in LDS: BKS-deep steps give rows of 2 * BKS bytes. The 16-B chunk c of row r is
+// stored at chunk c ^ swz(r), which makes every ds_read_b128 of an A fragment (16 rows x one chunk
+// per lane quarter) conflict-free: rows of 128 B (BKS = 64) XOR with r % 8, rows of 64 B
+// (BKS = 32) with 2 * ((r / 8) % 2) (searched exhaustively over the four lane groups).
+template <int BKS>
+ZK_DEV int pf_swz(int r) { return BKS == 64 ? (r & 7) : (((r >> 3) & 1) << 1); }
+template <int BKS>
+ZK_DEV int pf_a_off(int r, int c) { return r * (2 * BKS) + ((c ^ pf_swz<BKS>(r)) << 4); }
 
 template <int N_>
 ZK_DEV void pf_vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
@@ -65,49 +68,55 @@ ZK_DEV void pf_tile(int L, int nwg, int tm, int tn, int& bm, int& bn) {
     (void)gcols;
 }
 
-template <int MODE>
+// BKS: K depth of one LDS stage (32 or 64); NSTG: stages in the ring (NSTG - 1 in flight).
+template <int MODE, int BKS, int NSTG>
 __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__ A, long lda,
                                                       const bf16_t* __restrict__ W, int M, int N, int K,
                                                       float* __restrict__ C, bf16_t* __restrict__ Cb,
                                                       const int32_t* skip) {
+    constexpr int KSS = BKS / 32;                        // 32-deep MFMA k-slices per stage
+    constexpr int AST = PF_BM * BKS * 2, BST = PF_BN * BKS * 2, ST = AST + BST;
+    constexpr int RPP = 1024 / (2 * BKS);                // activation rows per 1 KB LDS-DMA piece
+    constexpr int CPR = 2 * BKS / 16;                    // 16-B chunks per activation row
+    constexpr int NA = AST / 1024 / 8, NB = BST / 1024 / 8;     // pieces per wave and stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip && *skip) return;
     const int tm = (M + PF_BM - 1) / PF_BM, tn = (N + PF_BN - 1) / PF_BN;
     int bm, bn;
     pf_tile(blockIdx.x, gridDim.x, tm, tn, bm, bn);
     const int m0 = bm * PF_BM, n0 = bn * PF_BN;
-    const int nk = K / PF_BK;
+    const int nk = K / BKS;
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ln = lane & 15, lg = lane >> 4;
     const int wr = w >> 2, wc = w & 3;
 
-    // ---- loader addresses: 4 activation pieces + 4 weight blocks of 1 KB per thread and step
-    // activation piece p = i * 8 + w covers tile rows 8p..8p+7: lane L -> row 8p + L/8, LDS slot L%8
-    // holding source chunk (L%8) ^ (row%8) (pf_lds_off's swizzle applied on the source address)
-    const bf16_t* asrc[4];
+    // ---- loader addresses. Activation piece p = i * 8 + w covers tile rows RPP p .. RPP p + RPP - 1:
+    // lane L lands at row RPP p + L / CPR, chunk slot L % CPR, which holds source chunk slot ^ swz(row)
+    const bf16_t* asrc[NA];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int p = i * 8 + w, row = 8 * p + (lane >> 3);
+    for (int i = 0; i < NA; ++i) {
+        const int p = i * 8 + w, row = RPP * p + lane / CPR;
         const int m = min(m0 + row, M - 1);            // rows >= M compute garbage that is never stored
-        asrc[i] = A + (size_t)m * lda + (((lane & 7) ^ (row & 7)) << 3);
+        asrc[i] = A + (size_t)m * lda + (((lane % CPR) ^ pf_swz<BKS>(row)) << 3);
     }
-    // weight block b = i * 8 + w: 16-column group g = b / 2, k-slice b % 2 of the step
-    const bf16_t* bsrc[4];
+    // weight block b = i * 8 + w: 16-column group b / KSS, k-slice b % KSS of the stage
+    const bf16_t* bsrc[NB];
     const int ntl = (N + 15) / 16;                      // packed 16-row tiles present (padded to 64 rows)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int b = i * 8 + w, g = n0 / 16 + (b >> 1);
+    for (int i = 0; i < NB; ++i) {
+        const int b = i * 8 + w, g = n0 / 16 + b / KSS;
         const int gg = g < ntl ? g : 0;                 // groups past N stream group 0 (never stored)
-        bsrc[i] = W + ((size_t)gg * (K >> 5) + (b & 1)) * 512 + lane * 8;
+        bsrc[i] = W + ((size_t)gg * (K >> 5) + (b % KSS)) * 512 + lane * 8;
     }
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + w * 1024);
     auto issue = [&](int kt, int st) {
-        const uint32_t sa = lds0 + st * PF_ST, sb = sa + PF_AST;
+        const uint32_t sa = lds0 + st * ST, sb = sa + AST;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pf_glds(asrc[i] + kt * PF_BK, sa + i * 8192);
+        for (int i = 0; i < NA; ++i) pf_glds(asrc[i] + kt * BKS, sa + i * 8192);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pf_glds(bsrc[i] + (size_t)kt * 1024, sb + i * 8192);
+        for (int i = 0; i < NB; ++i) pf_glds(bsrc[i] + (size_t)kt * KSS * 512, sb + i * 8192);
     };
+    constexpr int LPS = NA + NB;                         // LDS-DMA loads per wave and stage
 
     f32x4 acc[8][4];
 #pragma unroll
@@ -115,37 +124,45 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    issue(0, 0);
-    pf_vm_wait<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    for (int kt = 0; kt < nk; ++kt) {
-        // the other stage was last read in step kt - 1, which every wave finished before the
-        // barrier that ended it
-        if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-        const char* sa = smem + (kt & 1) * PF_ST;
-        const char* sb = sa + PF_AST;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+    for (int s0 = 0; s0 < NSTG - 1; ++s0)
+        if (s0 < nk) issue(s0, s0);
+    for (int kt = 0; kt < nk; ++kt) {
+        // step kt's copies: everything issued after them may stay in flight
+        const int after = min(NSTG - 2, nk - 1 - kt);
+        if constexpr (NSTG >= 4) {
+            if (after >= 2) pf_vm_wait<2 * LPS>();
+            else if (after == 1) pf_vm_wait<LPS>();
+            else pf_vm_wait<0>();
+        } else if constexpr (NSTG == 3) {
+            if (after >= 1) pf_vm_wait<LPS>();
+            else pf_vm_wait<0>();
+        } else {
+            pf_vm_wait<0>();
+        }
+        // the barrier publishes every wave's copies of step kt and ends every read of the stage the
+        // refill below overwrites (read in step kt - 1; this wave's reads retired here)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
+        const char* sa = smem + (kt % NSTG) * ST;
+        const char* sb = sa + AST;
+#pragma unroll
+        for (int ks = 0; ks < KSS; ++ks) {
             uint4 bf[4];
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
-                bf[nt] = *reinterpret_cast<const uint4*>(sb + (((wc * 4 + nt) * 2 + ks) << 10) + lane * 16);
+                bf[nt] = *reinterpret_cast<const uint4*>(sb + (((wc * 4 + nt) * KSS + ks) << 10) + lane * 16);
 #pragma unroll
             for (int mt = 0; mt < 8; ++mt) {
-                const uint4 a = *reinterpret_cast<const uint4*>(sa + pf_lds_off(wr * 128 + mt * 16 + ln, ks * 4 + lg));
+                const uint4 a = *reinterpret_cast<const uint4*>(sa + pf_a_off<BKS>(wr * 128 + mt * 16 + ln, ks * 4 + lg));
 #pragma unroll
                 for (int nt = 0; nt < 4; ++nt)
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(bf[nt]), acc[mt][nt], 0,
                                                                           0, 0);
             }
         }
-        // this wave's copies of step kt + 1 have landed and its reads of stage kt & 1 retired; the
-        // barrier publishes everyone's copies and ends every read of the stage the next step refills
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        pf_vm_wait<0>();
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
     }
 
     // ---- epilogue: acc[mt][nt][i] = C[m0 + wr*128 + mt*16 + lg*4 + i][n0 + wc*64 + nt*16 + ln]
@@ -186,16 +203,25 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
 
 // The prefill regime of zk_gemm_bf16 (split 1, large M): true when the 256 x 256 kernel takes the call.
 bool zk_gemm_pf_applies(int M, int N, int K, int nsplit) {
-    if (nsplit != 1 || K % PF_BK != 0 || N % 64 != 0) return false;
+    if (nsplit != 1 || K % 64 != 0 || N % 64 != 0) return false;
     const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + PF_BN - 1) / PF_BN);
     return tiles >= 256;                              // at least one tile per CU
 }
+
+// stage depth and ring length: 64-deep stages x 2 (default), or 32-deep x 4 (3 in flight; 128 KB either
+// way): 32 x 4 measured 2-4 % slower at the c3 prefill shapes (profiles/r4_prefill_gemm_bks_ab.txt), so the
+// kernel is not waiting on copy latency
+#ifndef ZK_PF_BKS
+#define ZK_PF_BKS 64
+#endif
+constexpr int PF_BKS = ZK_PF_BKS, PF_NSTG = PF_BKS == 64 ? 2 : 4;
+constexpr int PF_LDS = PF_NSTG * (PF_BM + PF_BN) * PF_BKS * 2;
 
 int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int mode, float* C, void* Cb,
                const int32_t* skip, void* stream) {
     const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + PF_BN - 1) / PF_BN);
     ZK_REQUIRE(tiles < (1L << 31), "zk_gemm_bf16 (prefill): too many tiles");
-    auto kern = mode == 0 ? &k_gemm_pf<0> : &k_gemm_pf<1>;
+    auto kern = mode == 0 ? &k_gemm_pf<0, PF_BKS, PF_NSTG> : &k_gemm_pf<1, PF_BKS, PF_NSTG>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
     hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(PF_NT), PF_LDS, (hipStream_t)stream, (const bf16_t*)A, lda,
                        (const bf16_t*)W, M, N, K, C, (bf16_t*)Cb, skip);
