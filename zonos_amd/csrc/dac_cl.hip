@@ -122,7 +122,16 @@ constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 // registers are sized for
 // NWY: position waves (2 compute waves per position range: the two channel halves), NLDK loader
 // waves: 2 x NWY + NLDK waves per workgroup.
-template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2, int NWY = 2, int NLDK = CL_NLD>
+// SPB: steps published per barrier -- the compute waves multiply SPB (tap, chunk) steps between two
+// barriers (a step is only FM x NQ MFMAs per wave, so a barrier per step holds the waves at the
+// barrier and the LDS read restart for a large share of the step); the rings hold 2 (SPB - 1) more
+// weight slots and the window ring ceil((DX + 2 SPB - 1) / ks) + 1 slots.
+#ifndef ZK_CL_SPB
+#define ZK_CL_SPB 1
+#endif
+constexpr int CL_SPB = ZK_CL_SPB;
+template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2, int NWY = 2, int NLDK = CL_NLD,
+          int SPB = CL_SPB>
 #ifndef ZK_CL_LBW
 #define ZK_CL_LBW(OCC_, NT_) ((OCC_ * (NT_) + 255) / 256)
 #endif
@@ -163,8 +172,11 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
     const int win = QTT + (ks - 1) * dil;
     const int nxp = (win + 15) >> 4;             // window pieces (16 rows each)
     const int XS = nxp * 1024;
+    // weight ring slots: the loader refills a slot at most 2 SPB steps after the barrier that let it
+    // run (it can be SPB steps ahead of the barrier it passed, the compute waves SPB behind it)
+    constexpr int NWS = DA + 2 * SPB;
     char* const wring = smem;
-    char* const xring = smem + (DA + 2) * WS;
+    char* const xring = smem + NWS * WS;
     const int nchunk = Cin / CI, nstep = nchunk * ks;
 
 #ifdef ZK_CL_PROF
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
                     }
                     nl += nwl;
                 }
-                if (++wslot == DA + 2) wslot = 0;
+                if (++wslot == NWS) wslot = 0;
                 if (++tw == ks) {
                     tw = 0;
                     if (++cw == nchunk) {
@@ -280,8 +292,8 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
 #pragma unroll
             for (int k = 0; k < DA; ++k) hist[k] = hist[k + 1];
             hist[DA] = nl;
-            if (j >= 0) {
-                // step j needs W(j), issued by iteration j - DA; everything issued later may stay in flight
+            if (j >= 0 && (j % SPB == SPB - 1 || j == total - 1)) {
+                // steps up to j need W(j), issued by iteration j - DA; everything issued later may stay in flight
                 int pend = 0;
 #pragma unroll
                 for (int k = 1; k <= DA; ++k) pend += hist[k];
@@ -338,8 +350,10 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
         }
 
         for (int s = 0; s < nstep; ++s) {
-            __builtin_amdgcn_s_barrier();            // step s is in LDS
-            asm volatile("" ::: "memory");
+            if (SPB == 1 || (it * nstep + s) % SPB == 0) {
+                __builtin_amdgcn_s_barrier();        // steps s .. s + SPB - 1 are in LDS
+                asm volatile("" ::: "memory");
+            }
             if (wv == 0 && it == 0) ZK_CL_STAMP(2, s);
 #ifdef ZK_CL_PROF
             if (it == 0 && s == 0 && wv == 0 && blockIdx.x < 64 && lane == 0)
@@ -347,7 +361,7 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
 #endif
             const char* xb = xring + xslot * XS;
             const char* wb = wring + wslot * WS;
-            if (++wslot == DA + 2) wslot = 0;
+            if (++wslot == NWS) wslot = 0;
             uint4 a[FM], bq[NQ];
 #pragma unroll
             for (int m = 0; m < FM; ++m)
@@ -772,14 +786,16 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
     const size_t ws = (size_t)32 * FM * 64;
     const int da = CL_DA;
     const size_t lds_cap = fat ? 160 * 1024 : 80 * 1024;
-    // window lead DX >= da steps, ring NX = 1 + ceil((DX+1)/ks) slots; keep LDS <= 80 KiB (2 per CU)
+    // window lead DX >= da steps, ring NX = 1 + ceil((DX + 2 SPB - 1)/ks) slots, weight ring da + 2 SPB;
+    // keep LDS <= 80 KiB (2 per CU)
     const size_t ept = (size_t)2 * 3 * 32 * FM * sizeof(float);      // epilogue constants tables (x 2)
-    int dx = std::max(da, ks), nx = 1 + (dx + 1 + ks - 1) / ks;
-    while (dx > da && (da + 2) * ws + nx * xs + ept > lds_cap) {
+    const int spb = CL_SPB, nws = da + 2 * spb;
+    int dx = std::max(da, ks), nx = 1 + (dx + 2 * spb - 1 + ks - 1) / ks;
+    while (dx > da && nws * ws + nx * xs + ept > lds_cap) {
         --dx;
-        nx = 1 + (dx + 1 + ks - 1) / ks;
+        nx = 1 + (dx + 2 * spb - 1 + ks - 1) / ks;
     }
-    const size_t lds = (da + 2) * ws + nx * xs + ept;
+    const size_t lds = nws * ws + nx * xs + ept;
     ZK_REQUIRE(lds <= 160 * 1024, "zk_dac_conv_cl: LDS %zu too large", lds);
     const int nq = (Qn + qt - 1) / qt;
     const long ntiles = (long)B * nq * (Cout / (32 * FM)) * nphase;
