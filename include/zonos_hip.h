@@ -409,6 +409,21 @@ int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* 
                    int out_stride, int out_off0, int Tout, const float* resid, float* x_out,
                    const float* alpha_next, void* s_out, int s_f32, const int32_t* lens, int in_scale,
                    int out_scale, void* stream);
+/* One whole DAC residual unit (modeling_dac.py:222-233, ResidualUnit.forward) in one launch:
+ *   y  = b7 + conv7_dil(s_in)                      (s_in = fp16 Snake_a1(x), [B][T][C])
+ *   s2 = fp16(Snake_a2(y));  v = x + b1 + W1 s2     (1x1 conv; the fp16 s2 never leaves the chip)
+ *   x[b][t][c] = v;  s_out[b][t][c] = fp16(Snake_{alpha_next}(v))  (s_f32 = 1: fp32, exact sinf)
+ * Replaces the pair zk_dac_conv_cl(k7 -> s2) + zk_dac_conv_cl(1x1, resid = x); the same masking
+ * (inputs at t >= lens[b]*scale read 0, outputs there written 0). w7 fp16 [7][C][C], w1 fp16
+ * [C][C] (zk_dac_prep_w16 layouts). s_out must not alias s_in. Built for C = 96; the 1x1 sums
+ * run on 16x16x16 MFMAs (a different fp32 summation grouping than the 32-deep unfused conv:
+ * results equal to rounding, not bit for bit). zk_dac_resunit_supported(C): 0 = not fused at this
+ * C, 1 = fused except the decode's last unit (the fp32-Snake one), 2 = every unit; zk_dac_decode
+ * and the Python-issued sequence both follow it. */
+int zk_dac_resunit_supported(int C);
+int zk_dac_resunit_cl(const uint16_t* s_in, int B, int C, int T, const uint16_t* w7, const float* b7, int dil,
+                      const float* a2, const uint16_t* w1, const float* b1, float* x, const float* alpha_next,
+                      void* s_out, int s_f32, const int32_t* lens, int scale, void* stream);
 /* out[b][t] = tanh(bias + sum_{c,k} w[c*7+k] * s[b][t+k-3][c]), 0 at t >= lens[b]*scale
  * (s = fp32 output of the final Snake, zk_dac_conv_cl with s_f32 = 1; modeling_dac.py:437-439). */
 int zk_dac_tail_cl(const float* s, int B, int C, int T, const float* w, const float* bias,

@@ -52,6 +52,14 @@ STUB(zk_dac_rvq_decode_cl, const int64_t*, int, int, int, long, const float*, in
 STUB(zk_dac_conv_cl, const uint16_t*, int, int, int, const uint16_t*, long, const float*, int, int, int, int, int, int,
      int, int, int, const float*, float*, const float*, void*, int, const int32_t*, int, int, void*)
 STUB(zk_dac_tail_cl, const float*, int, int, int, const float*, const float*, float*, const int32_t*, int, void*)
+static int g_alias = 0;             // fused residual units whose output buffer aliased their input
+extern "C" int zk_dac_resunit_supported(int C) { return C == 96 ? 1 : 0; }
+extern "C" int zk_dac_resunit_cl(const uint16_t* s_in, int, int, int, const uint16_t*, const float*, int, const float*,
+                                 const uint16_t*, const float*, float*, const float*, void* s_out, int,
+                                 const int32_t*, int, void*) {
+    g_alias += s_out == static_cast<const void*>(s_in);
+    return stub("zk_dac_resunit_cl");
+}
 
 // ---- internal entries of zonos_amd/csrc/warm.h (C++ linkage): a warm-up variant records as the launch it
 // replaces, so the per-layer launch counts below are the same with and without the L2 warm-up
@@ -209,8 +217,12 @@ static void dac() {
     g_calls.clear();
     CHECK(zk_dac_decode(&d, codes, 1, 43, nullptr, ws.data(), ws.size(), out, nullptr) == 0, "dac: %s",
           zk_last_error());
-    // rvq + conv1 + per block (ConvT + 3 x (k7 + 1x1)) + tail
-    CHECK(g_calls.size() == 1 + 1 + 4 * 7 + 1, "dac decode: %zu calls", g_calls.size());
+    // rvq + conv1 + per block (ConvT + 3 x (k7 + 1x1)) + tail; the 96-channel block's first two units
+    // fused (one launch each), never writing their input buffer
+    CHECK(g_calls.size() == 1 + 1 + 4 * 7 + 1 - 2, "dac decode: %zu calls", g_calls.size());
+    int nfused = 0;
+    for (const std::string& c : g_calls) nfused += c == "zk_dac_resunit_cl";
+    CHECK(nfused == 2 && g_alias == 0, "fused units %d, aliased %d", nfused, g_alias);
     CHECK(zk_dac_decode(&d, codes, 1, 43, nullptr, ws.data(), ws.size() - 1, out, nullptr) != 0 &&
               strstr(zk_last_error(), "workspace"), "small workspace must fail");
     zk_dac_desc nob = dac_desc(0);

@@ -112,6 +112,67 @@ def test_conv_cl_vs_torch(Cin, Cout, ks, dil, T, use_resid):
     assert (s32 - s_ref).abs().max().item() < 2e-3 * max(1.0, s_ref.abs().max().item())
 
 
+# the fused residual unit (zk_dac_resunit_cl, C = 96): 512-position tiles, one workgroup per CU;
+# T = 120000 at B = 3 gives 705 tiles, >= 2 per persistent workgroup
+@pytest.mark.parametrize("dil,T", [(1, 300), (3, 517), (9, 1000), (3, 120000)])
+def test_resunit_fused_vs_pair_and_torch(dil, T):
+    L = _lib()
+    C, B, dev = 96, 3, "cuda"
+    assert L.load().zk_dac_resunit_supported(192) == 0      # (96: the product fuses, variants may not)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    if T >= 100000:
+        assert B * (-(-T // 512)) >= 2 * ncu
+    torch.manual_seed(dil * 1000 + T)
+    st = L.stream_ptr(torch.device(dev))
+    lens = torch.tensor([T, T // 2, 1], dtype=torch.int32, device=dev)
+    s_in = torch.randn(B, T, C, device=dev).half()
+    x0 = torch.randn(B, T, C, device=dev)
+    w7 = (torch.randn(C, C, 7, device=dev) / math.sqrt(C * 7)).float()
+    w1 = (torch.randn(C, C, 1, device=dev) / math.sqrt(C)).float()
+    b7, b1 = torch.randn(C, device=dev) * 0.1, torch.randn(C, device=dev) * 0.1
+    a2, an = torch.rand(C, device=dev) + 0.5, torch.rand(C, device=dev) + 0.5
+    w7h, w1h = _prep(w7, 0), _prep(w1, 0)
+    # the unfused pair (k7 -> fp16 s2; 1x1 + residual -> x, next Snake)
+    tmp = torch.empty(B, T, C, dtype=torch.int16, device=dev)
+    x_pair, s_pair = x0.clone(), torch.empty(B, T, C, dtype=torch.int16, device=dev)
+    L.call("zk_dac_conv_cl", L.ptr(s_in), B, C, T, L.ptr(w7h), 0, L.ptr(b7), C, 7, dil, 3 * dil, T, 1, 1, 0, T,
+           None, None, L.ptr(a2), L.ptr(tmp), 0, L.ptr(lens), 1, 1, st)
+    L.call("zk_dac_conv_cl", L.ptr(tmp), B, C, T, L.ptr(w1h), 0, L.ptr(b1), C, 1, 1, 0, T, 1, 1, 0, T,
+           L.ptr(x_pair), L.ptr(x_pair), L.ptr(an), L.ptr(s_pair), 0, L.ptr(lens), 1, 1, st)
+    # fused, fp16 and fp32 Snake outputs
+    x_f, s_f = x0.clone(), torch.full((B, T, C), 12345, dtype=torch.int16, device=dev)
+    L.call("zk_dac_resunit_cl", L.ptr(s_in), B, C, T, L.ptr(w7h), L.ptr(b7), dil, L.ptr(a2), L.ptr(w1h), L.ptr(b1),
+           L.ptr(x_f), L.ptr(an), L.ptr(s_f), 0, L.ptr(lens), 1, st)
+    x_f32, s_f32 = x0.clone(), torch.empty(B, T, C, device=dev)
+    L.call("zk_dac_resunit_cl", L.ptr(s_in), B, C, T, L.ptr(w7h), L.ptr(b7), dil, L.ptr(a2), L.ptr(w1h), L.ptr(b1),
+           L.ptr(x_f32), L.ptr(an), L.ptr(s_f32), 1, L.ptr(lens), 1, st)
+    with pytest.raises(L.ZonosHipError, match="alias"):
+        L.call("zk_dac_resunit_cl", L.ptr(s_in), B, C, T, L.ptr(w7h), L.ptr(b7), dil, L.ptr(a2), L.ptr(w1h),
+               L.ptr(b1), L.ptr(x_f32), L.ptr(an), L.ptr(s_in), 0, L.ptr(lens), 1, st)
+    torch.cuda.synchronize()
+    # fused vs pair: the same k7 sums; the 1x1 sums grouped 16- instead of 32-deep (fp32 rounding only)
+    scale = max(1.0, x_pair.abs().max().item())
+    assert (x_f - x_pair).abs().max().item() < 1e-5 * scale
+    assert torch.equal(x_f, x_f32)
+    sp, sf = s_pair.view(torch.float16).float(), s_f.view(torch.float16).float()
+    assert (sf - sp).abs().max().item() < 2e-3 * max(1.0, sp.abs().max().item())
+    assert (sf != sp).float().mean().item() < 1e-3
+    for b in range(B):
+        assert torch.all(x_f[b, int(lens[b]):] == 0) and torch.all(sf[b, int(lens[b]):] == 0)
+    # fp32 torch reference of the unit on the same fp16 operands
+    xin = s_in.float().clone()
+    for b in range(B):
+        xin[b, int(lens[b]):] = 0
+    y = F.conv1d(xin.transpose(1, 2), w7.half().float(), b7, padding=3 * dil, dilation=dil).transpose(1, 2)
+    s2 = _snake(y, a2).half().float()
+    v = x0 + (s2 @ w1[:, :, 0].half().float().t() + b1)
+    for b in range(B):
+        v[b, int(lens[b]):] = 0
+    assert (x_f - v).abs().max().item() < 2e-3 * max(1.0, v.abs().max().item())
+    s_ref = _snake(v, an)
+    assert (s_f32 - s_ref).abs().max().item() < 2e-3 * max(1.0, s_ref.abs().max().item())
+
+
 @pytest.mark.parametrize("Cin,Cout,st,T", [(192, 96, 2, 70), (1536, 768, 8, 12), (384, 192, 4, 33),
                                           (192, 96, 2, 40000), (768, 384, 4, 9000)])
 def test_convt_cl_vs_torch(Cin, Cout, st, T):

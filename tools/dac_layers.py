@@ -25,6 +25,18 @@ orig = autoencoder.call
 
 
 def timed(name, *args):
+    if name == "zk_dac_resunit_cl":          # fused residual unit: k7 + 1x1 flops
+        B, Cc, T = args[1], args[2], args[3]
+        orig("zk_event_record", e0.value, S)
+        r = orig(name, *args)
+        orig("zk_event_record", e1.value, S)
+        ms = C.c_float()
+        orig("zk_event_elapsed_ms", e0.value, e1.value, C.byref(ms))
+        key = (Cc, Cc, 8, T, 1)              # "taps 8" = the fused unit (7 + 1)
+        rows[key][0] += 1
+        rows[key][1] += ms.value
+        rows[key][2] += 2.0 * Cc * Cc * 8 * T * B
+        return r
     if name != "zk_dac_conv_cl":
         return orig(name, *args)
     Cin, Tin, Cout, ks, Qn, nphase_stride = args[2], args[3], args[7], args[8], args[11], args[5]

@@ -134,6 +134,7 @@ _SIGS = {
     "zk_dac_rvq_decode_cl": [P, I, I, I, L, P, I, I, I, P, P, P],
     "zk_dac_conv_cl": [P, I, I, I, P, L, P, I, I, I, I, I, I, I, I, I, P, P, P, P, I, P, I, I, P],
     "zk_dac_tail_cl": [P, I, I, I, P, P, P, P, I, P],
+    "zk_dac_resunit_cl": [P, I, I, I, P, P, I, P, P, P, P, P, P, I, P, I, P],
     "zk_dac_enc_conv1": [P, I, I, P, P, P, I, I, P, P, P],
     "zk_dac_rvq_encode": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P],
     "zk_resample": [P, I, L, P, I, I, I, I, P, L, P],
@@ -169,13 +170,15 @@ def load():
     lib.zk_abi_size.argtypes = [I]
     lib.zk_dac_decode_workspace.restype = C.c_size_t
     lib.zk_dac_decode_workspace.argtypes = [C.POINTER(DacDesc), I, I]
+    lib.zk_dac_resunit_supported.restype = C.c_int
+    lib.zk_dac_resunit_supported.argtypes = [I]
     _lib = lib
     return lib
 
 
 def exported_symbols() -> list[str]:
     return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_abi_size",
-                          "zk_dac_decode_workspace"]
+                          "zk_dac_decode_workspace", "zk_dac_resunit_supported"]
 
 
 def call(name: str, *args):

@@ -174,6 +174,9 @@ class HipDacDecoder:
     # the decode's launch sequence is enqueued by the C ABI (zk_dac_decode); False issues the
     # same sequence from Python (bit-identical; the reference for the test)
     c_dac = True
+    # Python-issued sequence: residual units fused where zk_dac_resunit_supported says so, as in
+    # zk_dac_decode; False = every unit as two convs (tests only)
+    fuse_units = True
 
     def _dac_desc(self):
         if getattr(self, "_desc", None) is None:
@@ -246,9 +249,18 @@ class HipDacDecoder:
                     a_next = blocks[bi + 1]["alpha"]
                 else:
                     a_next = cl["final_alpha"]
+                last = j + 1 == nres and bi + 1 == len(blocks)
+                fm = _lib.load().zk_dac_resunit_supported(cout) if self.fuse_units else 0
+                if fm == 2 or (fm == 1 and not last):
+                    # the whole unit in one launch, into the other buffer (the k7 reads its input's halo)
+                    out = torch.empty(B, L, cout, device=dev) if last else tmp
+                    call("zk_dac_resunit_cl", ptr(act), B, cout, L, ptr(ru["w1"]), ptr(ru["b1"]), d, ptr(ru["a2"]),
+                         ptr(ru["w2"]), ptr(ru["b2"]), ptr(x), ptr(a_next), ptr(out), int(last), ptr(lens), scale,
+                         stream)
+                    act, tmp = out, act
+                    continue
                 call("zk_dac_conv_cl", ptr(act), B, cout, L, ptr(ru["w1"]), 0, ptr(ru["b1"]), cout, 7, d, 3 * d, L,
                      1, 1, 0, L, None, None, ptr(ru["a2"]), ptr(tmp), 0, ptr(lens), scale, scale, stream)
-                last = j + 1 == nres and bi + 1 == len(blocks)
                 if last:       # the tail's input: fp32 Snake output (keeps the waveform at fp32-level error)
                     act = torch.empty(B, L, cout, device=dev)
                 call("zk_dac_conv_cl", ptr(tmp), B, cout, L, ptr(ru["w2"]), 0, ptr(ru["b2"]), cout, 1, 1, 0, L,

@@ -430,27 +430,32 @@ extern "C" int zk_dac_decode(const zk_dac_desc* d, const int64_t* codes, int B, 
     }
     char* ws = static_cast<char*>(workspace);
     uint16_t* z = reinterpret_cast<uint16_t*>(ws + p.z);
-    uint16_t* bufs[2] = {reinterpret_cast<uint16_t*>(ws + p.a), reinterpret_cast<uint16_t*>(ws + p.b)};
+    // three fp16 activation buffers; each conv writes one its input is not in (a fused residual unit
+    // reads its input's neighbours as the k7 halo, so it never writes in place)
+    uint16_t* bufs[3] = {reinterpret_cast<uint16_t*>(ws + p.a), reinterpret_cast<uint16_t*>(ws + p.b),
+                         reinterpret_cast<uint16_t*>(ws + p.tmp)};
+    auto other = [&](const void* u, const void* v) -> uint16_t* {
+        for (uint16_t* c : bufs)
+            if (c != u && c != v) return c;
+        return nullptr;
+    };
     float* x = reinterpret_cast<float*>(ws + p.x);
-    uint16_t* tmp = reinterpret_cast<uint16_t*>(ws + p.tmp);
     float* last_act = reinterpret_cast<float*>(ws + p.last);
     ZK_DSTEP(zk_dac_rvq_decode_cl(codes, B, d->ncb, T, (long)d->ncb * T, d->tables, d->codebook_size, d->hidden,
                                   d->cin0, z, lens, stream));
     const float* a_next = d->nblocks ? d->blocks[0].alpha : d->final_alpha;
-    int cur = 0;
     ZK_DSTEP(zk_dac_conv_cl(z, B, d->cin0, T, d->conv1_w, 0, d->conv1_b, d->c0, 7, 1, 3, T, 1, 1, 0, T, nullptr,
-                            nullptr, a_next, bufs[cur], 0, lens, 1, 1, stream));
+                            nullptr, a_next, bufs[0], 0, lens, 1, 1, stream));
     int L = T, scale = 1, cch = d->c0;
-    const void* act = bufs[cur];
+    const void* act = bufs[0];
     bool act_f32 = false;
     for (int bi = 0; bi < d->nblocks; ++bi) {
         const zk_dac_block& k = d->blocks[bi];
         const int st = k.stride, Lo = L * st;
-        uint16_t* s_new = bufs[cur ^ 1];
+        uint16_t* s_new = other(act, nullptr);
         ZK_DSTEP(zk_dac_conv_cl(static_cast<const uint16_t*>(act), B, k.cin, L, k.wt, 2L * k.cout * k.cin, k.bt,
                                 k.cout, 2, 1, 1, L + 1, st, st, -((st + 1) / 2), Lo, nullptr, x, k.res[0].a1, s_new, 0,
                                 lens, scale, scale * st, stream));
-        cur ^= 1;
         act = s_new;
         scale *= st;
         L = Lo;
@@ -458,17 +463,25 @@ extern "C" int zk_dac_decode(const zk_dac_desc* d, const int64_t* codes, int B, 
             const zk_dac_resunit& ru = k.res[j];
             const float* an = j + 1 < k.nres ? k.res[j + 1].a1 : (bi + 1 < d->nblocks ? d->blocks[bi + 1].alpha
                                                                                            : d->final_alpha);
-            ZK_DSTEP(zk_dac_conv_cl(static_cast<const uint16_t*>(act), B, k.cout, L, ru.w1, 0, ru.b1, k.cout, 7,
-                                    ru.dil, 3 * ru.dil, L, 1, 1, 0, L, nullptr, nullptr, ru.a2, tmp, 0, lens, scale,
-                                    scale, stream));
             const bool last = j + 1 == k.nres && bi + 1 == d->nblocks;
-            void* s_out = last ? static_cast<void*>(last_act) : const_cast<void*>(act);
-            ZK_DSTEP(zk_dac_conv_cl(tmp, B, k.cout, L, ru.w2, 0, ru.b2, k.cout, 1, 1, 0, L, 1, 1, 0, L, x, x, an, s_out,
-                                    last ? 1 : 0, lens, scale, scale, stream));
-            if (last) {
-                act = last_act;
-                act_f32 = true;
+            uint16_t* tmp = other(act, nullptr);
+            const int fm = zk_dac_resunit_supported(k.cout);
+            if (fm == 2 || (fm == 1 && !last)) {
+                // the whole unit in one launch (k7 -> Snake -> 1x1 -> + x -> next Snake)
+                void* s_out = last ? static_cast<void*>(last_act) : static_cast<void*>(tmp);
+                ZK_DSTEP(zk_dac_resunit_cl(static_cast<const uint16_t*>(act), B, k.cout, L, ru.w1, ru.b1, ru.dil,
+                                           ru.a2, ru.w2, ru.b2, x, an, s_out, last ? 1 : 0, lens, scale, stream));
+                act = s_out;
+            } else {
+                ZK_DSTEP(zk_dac_conv_cl(static_cast<const uint16_t*>(act), B, k.cout, L, ru.w1, 0, ru.b1, k.cout, 7,
+                                        ru.dil, 3 * ru.dil, L, 1, 1, 0, L, nullptr, nullptr, ru.a2, tmp, 0, lens,
+                                        scale, scale, stream));
+                void* s_out = last ? static_cast<void*>(last_act) : const_cast<void*>(act);
+                ZK_DSTEP(zk_dac_conv_cl(tmp, B, k.cout, L, ru.w2, 0, ru.b2, k.cout, 1, 1, 0, L, 1, 1, 0, L, x, x, an,
+                                        s_out, last ? 1 : 0, lens, scale, scale, stream));
+                act = s_out;
             }
+            if (last) act_f32 = true;
         }
         cch = k.cout;
     }

@@ -48,6 +48,8 @@ struct Img {                      // [rows][CI fp16] image, 16-B groups XOR-swiz
 };
 
 ZK_DEV f16x8 as_h8(uint4 v) { return __builtin_bit_cast(f16x8, v); }
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+ZK_DEV f16x4 as_h4(uint2 v) { return __builtin_bit_cast(f16x4, v); }
 
 ZK_DEV float snake(float x, float a) {     // x + 1/(a + 1e-9) * sin(a x)^2   (modeling_dac.py:95-100)
     const float s = sinf(__fmul_rn(a, x));
@@ -130,23 +132,37 @@ constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 #define ZK_CL_SPB 1
 #endif
 constexpr int CL_SPB = ZK_CL_SPB;
+#ifndef ZK_RU_DEPHASE
+#define ZK_RU_DEPHASE 0              // fused unit at OCC 2: the second workgroup round starts this many 10-ns ticks late
+#endif
+// NWM: channel waves (2: the two channel halves; 1: every wave holds all CO_T channels of its
+// positions). FUSE (NWM = 1, one channel tile = all C channels): a whole residual unit in one
+// launch -- the k7 conv's accumulators, Snake'd to fp16, are already the B operands of
+// v_mfma_f32_16x16x16_f16 (lane (p, g) holds channels 4g..4g+3 of position p), so the 1x1 conv
+// multiplies them in registers against the C x C weights staged once in LDS, adds the residual
+// and writes x and the next Snake: the fp16 intermediate never goes to HBM (4 of the unit's 16 B
+// per element) and the 1x1 conv's launch, rings and barriers are gone.
 template <int FM, bool SF32, bool RES, int NQ, int DA = CL_DA, int OCC = 2, int NWY = 2, int NLDK = CL_NLD,
-          int SPB = CL_SPB>
+          int SPB = CL_SPB, int NWM = 2, bool FUSE = false>
 #ifndef ZK_CL_LBW
 #define ZK_CL_LBW(OCC_, NT_) ((OCC_ * (NT_) + 255) / 256)
 #endif
-__global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY + NLDK))) void k_conv_cl(
+__global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM * NWY + NLDK))) void k_conv_cl(
     const uint16_t* __restrict__ in, int Cin, int Tin, const uint16_t* __restrict__ w, long wphase,
     const float* __restrict__ bias, int Cout, int ks, int dil, int pad, int Qn, int nphase, int out_stride,
     int out_off0, int Tout, const float* resid, float* xout, const float* __restrict__ alpha,
     void* __restrict__ sout, int s_f32, const int32_t* __restrict__ lens, int in_scale, int out_scale, int nq,
-    int nx_slots, int dx, int B) {
+    int nx_slots, int dx, int B, const uint16_t* __restrict__ w1x1, const float* __restrict__ b1x1,
+    const float* __restrict__ alpha_out) {
     constexpr int CI = 32;
     using I = Img<CI>;
-    constexpr int CO_T = 32 * FM;
+    constexpr int CO_T = 16 * FM * NWM;
     constexpr int WS = CO_T * I::RB;             // weight slot bytes
     constexpr int NWP = CO_T / 16;               // weight pieces (1 KiB = 16 rows) per step
-    constexpr int NCW = 2 * NWY;                 // compute waves
+    constexpr int NCW = NWM * NWY;               // compute waves
+    static_assert(!FUSE || (NWM == 1 && !RES), "fused residual unit: one channel wave, residual in the epilogue");
+    constexpr int W1S = CO_T + 8;                // fused: 1x1 weight image row stride (halves)
+    constexpr bool W1LDS = FUSE && OCC == 1;     // fused, one workgroup per CU: 1x1 weights in LDS (else L1)
     constexpr int QTT = 16 * NQ * NWY;           // positions per tile
     extern __shared__ __attribute__((aligned(16))) char smem[];   // [W ring][X ring][epilogue tables x 2]
 
@@ -190,6 +206,14 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
         g_clprof_rt[blockIdx.x][4] = __builtin_amdgcn_s_memtime();
     }
 #endif
+    if constexpr (FUSE && OCC == 2 && ZK_RU_DEPHASE > 0) {
+        // the second round of workgroups (the one sharing CUs with the first) starts late, so a CU's
+        // two workgroups alternate between the MFMA-bound main loop and the HBM-bound epilogue
+        if (kx >= nper / 2) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ZK_RU_DEPHASE) __builtin_amdgcn_s_sleep(8);
+        }
+    }
     if (wv >= NCW) {
         // ---------------- loader waves: loader lw moves the pieces p with p % NLDK == lw
         // wave-uniform (readfirstlane): the piece counts and the vmcnt switch below stay scalar;
@@ -306,9 +330,20 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
         return;
     }
 
-    // ---------------- compute waves 0 .. NCW-1: 2 (co) x NWY (positions)
+    // ---------------- compute waves 0 .. NCW-1: NWM (co) x NWY (positions)
     const int ln = lane & 15, lg = lane >> 4, wm = wv / NWY, wn = wv % NWY;
     int t = 0, xslot = 0, wslot = 0;             // tap, window ring slot, weight ring slot of the step
+    constexpr int NE = FUSE ? 6 : 3;             // epilogue constant tables per tile
+    // fused: the 1x1 weights [co][ci] as an LDS image (row stride W1S halves), staged once per
+    // workgroup; visible to every compute wave after the first step barrier
+    uint16_t* const w1img = reinterpret_cast<uint16_t*>(xring + nx_slots * XS + 2 * NE * CO_T * sizeof(float));
+    if constexpr (W1LDS) {
+        for (int i = tid; i < CO_T * CO_T / 8; i += 64 * NCW) {
+            const int row = i / (CO_T / 8), c8 = i % (CO_T / 8);
+            *reinterpret_cast<uint4*>(w1img + row * W1S + c8 * 8) =
+                *reinterpret_cast<const uint4*>(w1x1 + (size_t)row * CO_T + c8 * 8);
+        }
+    }
     for (int it = 0; it < nt; ++it) {
         int b, phase, co0, q0;
         tile_of(it, b, phase, co0, q0);
@@ -322,12 +357,18 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
         // staged into an LDS table (two, by tile parity: a wave may still read the previous tile's)
         // while the steps run (the epilogue used to start with their global loads and four IEEE
         // divisions per channel quartet)
-        float* const ept = reinterpret_cast<float*>(xring + nx_slots * XS) + (it & 1) * 3 * CO_T;
+        float* const ept = reinterpret_cast<float*>(xring + nx_slots * XS) + (it & 1) * NE * CO_T;
         for (int i = tid; i < CO_T; i += 64 * NCW) {
-            const float a_ = sout ? alpha[co0 + i] : 1.f;
+            const float a_ = (FUSE || sout) ? alpha[co0 + i] : 1.f;
             ept[i] = bias[co0 + i];
             ept[CO_T + i] = a_;
             ept[2 * CO_T + i] = __fdiv_rn(1.0f, __fadd_rn(a_, 1e-9f));
+            if constexpr (FUSE) {
+                const float an = alpha_out[i];
+                ept[3 * CO_T + i] = b1x1[i];
+                ept[4 * CO_T + i] = an;
+                ept[5 * CO_T + i] = __fdiv_rn(1.0f, __fadd_rn(an, 1e-9f));
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            // visible after the next barrier
         const int len_out = lens ? lens[b] * out_scale : Tout;
@@ -401,6 +442,82 @@ __global__ __launch_bounds__(64 * (2 * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (2 * NWY
 #endif
         // acc[m][n][i] = C[co = co0 + wm*16FM + 16m + 4lg + i][q = q0 + 16NQ wn + 16n + ln]
         const int out_off = out_off0 + phase;
+        if constexpr (FUSE) {
+            // s2 = fp16(Snake_a2(conv7 + b7)) in the accumulator layout = the 16x16x16 B fragments
+            uint2 h[FM][NQ];
+#pragma unroll
+            for (int m = 0; m < FM; ++m) {
+                const int cl = m * 16 + lg * 4;
+                const float4 bb = *reinterpret_cast<const float4*>(ept + cl);
+                const float4 aa = *reinterpret_cast<const float4*>(ept + CO_T + cl);
+                const float4 rr = *reinterpret_cast<const float4*>(ept + 2 * CO_T + cl);
+#pragma unroll
+                for (int n = 0; n < NQ; ++n)
+                    h[m][n] = pack_h4(snake_fast(__fadd_rn(acc[m][n][0], bb.x), aa.x, rr.x),
+                                      snake_fast(__fadd_rn(acc[m][n][1], bb.y), aa.y, rr.y),
+                                      snake_fast(__fadd_rn(acc[m][n][2], bb.z), aa.z, rr.z),
+                                      snake_fast(__fadd_rn(acc[m][n][3], bb.w), aa.w, rr.w));
+            }
+            // residual rows of output block mo (clamped loads; out-of-range positions are not stored),
+            // one block ahead of the block being multiplied
+            float4 xr[2][NQ];
+            auto load_x = [&](int mo, int buf) {
+#pragma unroll
+                for (int n = 0; n < NQ; ++n) {
+                    const int q = q0 + wn * 16 * NQ + n * 16 + ln;
+                    const int tt = min(max(q * out_stride + out_off, 0), Tout - 1);
+                    xr[buf][n] = *reinterpret_cast<const float4*>(resid + ((size_t)b * Tout + tt) * Cout + mo * 16 + lg * 4);
+                }
+            };
+            load_x(0, 0);
+            // the 1x1 weight fragments are loaded per output block (L1-resident), not hoisted out of
+            // the tile loop into 72 registers held across the main loop
+            const uint16_t* w1p = w1x1;
+            asm volatile("" : "+s"(w1p));
+#pragma unroll
+            for (int mo = 0; mo < FM; ++mo) {
+                if (mo + 1 < FM) load_x(mo + 1, (mo + 1) & 1);
+                f32x4 z[NQ];
+#pragma unroll
+                for (int n = 0; n < NQ; ++n) z[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int m = 0; m < FM; ++m) {
+                    const uint2 wa = W1LDS ? *reinterpret_cast<const uint2*>(w1img + (mo * 16 + ln) * W1S + m * 16 + lg * 4)
+                                           : *reinterpret_cast<const uint2*>(w1p + (mo * 16 + ln) * CO_T + m * 16 + lg * 4);
+#pragma unroll
+                    for (int n = 0; n < NQ; ++n)
+                        z[n] = __builtin_amdgcn_mfma_f32_16x16x16f16(as_h4(wa), as_h4(h[m][n]), z[n], 0, 0, 0);
+                }
+                const int co = mo * 16 + lg * 4;
+                const float4 bb = *reinterpret_cast<const float4*>(ept + 3 * CO_T + co);
+                const float4 aa = *reinterpret_cast<const float4*>(ept + 4 * CO_T + co);
+                const float4 rr = *reinterpret_cast<const float4*>(ept + 5 * CO_T + co);
+#pragma unroll
+                for (int n = 0; n < NQ; ++n) {
+                    const int q = q0 + wn * 16 * NQ + n * 16 + ln;
+                    const int tt = q * out_stride + out_off;
+                    if (q >= Qn || tt < 0 || tt >= Tout) continue;
+                    const size_t o = ((size_t)b * Tout + tt) * Cout + co;
+                    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+                    if (tt < len_out) {
+                        const float4 r = xr[mo & 1][n];
+                        v0 = __fadd_rn(r.x, __fadd_rn(z[n][0], bb.x));
+                        v1 = __fadd_rn(r.y, __fadd_rn(z[n][1], bb.y));
+                        v2 = __fadd_rn(r.z, __fadd_rn(z[n][2], bb.z));
+                        v3 = __fadd_rn(r.w, __fadd_rn(z[n][3], bb.w));
+                    }
+                    *reinterpret_cast<float4*>(xout + o) = make_float4(v0, v1, v2, v3);
+                    if (SF32)
+                        reinterpret_cast<float4*>(sout)[o >> 2] =
+                            make_float4(snake(v0, aa.x), snake(v1, aa.y), snake(v2, aa.z), snake(v3, aa.w));
+                    else
+                        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(sout) + o) =
+                            pack_h4(snake_fast(v0, aa.x, rr.x), snake_fast(v1, aa.y, rr.y),
+                                    snake_fast(v2, aa.z, rr.z), snake_fast(v3, aa.w, rr.w));
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int m = 0; m < FM; ++m) {
             const int cl = wm * 16 * FM + m * 16 + lg * 4, co = co0 + cl;
@@ -705,7 +822,53 @@ int launch_conv(long ntiles, size_t lds, hipStream_t st, const uint16_t* in, int
     const long grid = std::min<long>((ntiles + 7) / 8 * 8, std::max<long>(resident, 8));
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, in, Cin, Tin, w, wphase, bias, Cout, ks,
                        dil, pad, Qn, nphase, out_stride, out_off0, Tout, resid, xout, alpha, sout, s_f32, lens,
-                       in_scale, out_scale, nq, nx, dx, B);
+                       in_scale, out_scale, nq, nx, dx, B, nullptr, nullptr, nullptr);
+    return 0;
+}
+
+// The fused residual unit at C = 96: position waves each holding all 96 channels x 64 positions
+// (FM = 6, NQ = 4), persistent like launch_conv. ZK_RU_OCC 1: one workgroup per CU of 8 position
+// waves (512-position tiles) + 4 loaders, the 1x1 weights in LDS; 2: two workgroups per CU of 4
+// position waves (256 positions) + 2 loaders, the 1x1 weights read through L1 -- one workgroup's
+// HBM-heavy epilogue (x in, x and s out: 10 B per element) then runs beside the other's MFMAs.
+#ifndef ZK_RU_OCC
+#define ZK_RU_OCC 1
+#endif
+constexpr int RU_C = 96, RU_FM = 6, RU_NQ = 4, RU_OCC = ZK_RU_OCC, RU_NWY = RU_OCC == 1 ? 8 : 4,
+              RU_NLD = RU_OCC == 1 ? 4 : 2;
+template <bool SF32>
+int launch_resunit(const uint16_t* s_in, int B, int T, const uint16_t* w7, const float* b7, int dil, const float* a2,
+                   const uint16_t* w1, const float* b1, float* x, const float* alpha_next, void* s_out,
+                   const int32_t* lens, int scale, hipStream_t st) {
+    constexpr int NT = 64 * (RU_NWY + RU_NLD);
+    constexpr int qt = 16 * RU_NQ * RU_NWY;
+    auto kern = &k_conv_cl<RU_FM, SF32, false, RU_NQ, CL_DA, RU_OCC, RU_NWY, RU_NLD, CL_SPB, 1, true>;
+    const int ks = 7, win = qt + (ks - 1) * dil;
+    const size_t xs = (size_t)((win + 15) / 16) * 1024, ws = (size_t)RU_C * 64;
+    const size_t fixed = (size_t)2 * 6 * RU_C * sizeof(float) + (RU_OCC == 1 ? (size_t)RU_C * (RU_C + 8) * 2 : 0);
+    const size_t cap = RU_OCC == 1 ? 160 * 1024 : 80 * 1024;
+    const int spb = CL_SPB, nws = CL_DA + 2 * spb;
+    int dx = std::max(CL_DA, ks), nx = 1 + (dx + 2 * spb - 1 + ks - 1) / ks;
+    while (dx > CL_DA && nws * ws + nx * xs + fixed > cap) {
+        --dx;
+        nx = 1 + (dx + 2 * spb - 1 + ks - 1) / ks;
+    }
+    const size_t lds = nws * ws + nx * xs + fixed;
+    ZK_REQUIRE(lds <= cap, "zk_dac_resunit_cl: LDS %zu too large (dil %d)", lds, dil);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int dev = 0, ncu = 0, occ = 0;
+    ZK_HIP(hipGetDevice(&dev));
+    ZK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    ZK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kern), NT, lds));
+    ZK_REQUIRE(occ >= 1, "zk_dac_resunit_cl: kernel does not fit a CU (LDS %zu)", lds);
+    const int nq = (T + qt - 1) / qt;
+    const long ntiles = (long)B * nq;
+    ZK_REQUIRE(ntiles < (1L << 31), "zk_dac_resunit_cl: too many tiles");
+    const long resident = (long)ncu * occ / 8 * 8;
+    const long grid = std::min<long>((ntiles + 7) / 8 * 8, std::max<long>(resident, 8));
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, s_in, RU_C, T, w7, 0L, b7, RU_C, ks, dil,
+                       3 * dil, T, 1, 1, 0, T, x, x, a2, s_out, (int)SF32, lens, scale, scale, nq, nx, dx, B, w1, b1,
+                       alpha_next);
     return 0;
 }
 
@@ -818,6 +981,31 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
 #undef ZK_CLF
 #undef ZK_CL
     ZK_CHECK_LAUNCH("zk_dac_conv_cl");
+    return 0;
+}
+
+// ZK_DAC_FUSE: 0 = every residual unit as two convs; 1 = the units of C = 96 fused except the last
+// (its fp32 Snake output makes the fused epilogue spill); 2 = the last one too
+#ifndef ZK_DAC_FUSE
+#define ZK_DAC_FUSE 1
+#endif
+extern "C" int zk_dac_resunit_supported(int C) { return C == RU_C ? ZK_DAC_FUSE : 0; }
+
+extern "C" int zk_dac_resunit_cl(const uint16_t* s_in, int B, int C, int T, const uint16_t* w7, const float* b7,
+                                 int dil, const float* a2, const uint16_t* w1, const float* b1, float* x,
+                                 const float* alpha_next, void* s_out, int s_f32, const int32_t* lens, int scale,
+                                 void* stream) {
+    ZK_REQUIRE(C == RU_C, "zk_dac_resunit_cl: C=%d (the fused unit is built for C = %d)", C, RU_C);
+    ZK_REQUIRE(dil >= 1 && 6 * dil <= MAXSPAN, "zk_dac_resunit_cl: dil=%d", dil);
+    ZK_REQUIRE(s_in != nullptr && w7 && b7 && a2 && w1 && b1 && x && alpha_next && s_out,
+               "zk_dac_resunit_cl: null argument");
+    ZK_REQUIRE(s_out != static_cast<const void*>(s_in),
+               "zk_dac_resunit_cl: s_out must not alias s_in (neighbouring tiles read it as their halo)");
+    if (B == 0 || T <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (s_f32) ZK_TRY(launch_resunit<true>(s_in, B, T, w7, b7, dil, a2, w1, b1, x, alpha_next, s_out, lens, scale, st));
+    else ZK_TRY(launch_resunit<false>(s_in, B, T, w7, b7, dil, a2, w1, b1, x, alpha_next, s_out, lens, scale, st));
+    ZK_CHECK_LAUNCH("zk_dac_resunit_cl");
     return 0;
 }
 

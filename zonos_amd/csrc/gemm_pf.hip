@@ -205,121 +205,6 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
     pf_epilogue<MODE>(acc, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
 }
 
-// The same tile and stages (BKS = 64, two 64 KB stages), each 64-deep step split into four phases
-// -- one C quadrant (64 rows x 32 columns of the wave's 128 x 64: 16 MFMAs) per phase -- and the two
-// wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7; one wave of each per SIMD) staggered by one
-// barrier: between two barriers one group reads the next quadrant's fragments from LDS while the
-// other multiplies, so each SIMD's MFMA pipe alternates between its two waves instead of idling
-// through every wave's LDS reads (the schedule of cdna_hip_programming.md's 256^2 8-phase template).
-// Quadrant order (rows, cols) (0,0) (0,1) (1,1) (1,0): the A fragments of a row half are read once
-// per step, the B fragments of column half 0 twice.
-// Stage protocol (barrier count b; group 0 reads phase p of step k between b = 8k+2p-1 and 8k+2p,
-// group 1 one barrier later): every wave issues its copies of step k+1 in its first read section of
-// step k (the stage they overwrite held step k-1, whose last reads -- group 1's phase 3 -- ended at
-// b = 8k-1) and waits for them in its last read section of step k, before b = 8k+6 (group 0) / 8k+7
-// (group 1), both ahead of group 0's first read of step k+1 (after b = 8k+7).
-template <int MODE>
-__global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf8(const bf16_t* __restrict__ A, long lda,
-                                                       const bf16_t* __restrict__ W, int M, int N, int K,
-                                                       float* __restrict__ C, bf16_t* __restrict__ Cb,
-                                                       const int32_t* skip) {
-    constexpr int BKS = 64;
-    constexpr int AST = PF_BM * BKS * 2, BST = PF_BN * BKS * 2, ST = AST + BST;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (skip && *skip) return;
-    const int tm = (M + PF_BM - 1) / PF_BM, tn = (N + PF_BN - 1) / PF_BN;
-    int bm, bn;
-    pf_tile(blockIdx.x, gridDim.x, tm, tn, bm, bn);
-    const int m0 = bm * PF_BM, n0 = bn * PF_BN;
-    const int nk = K / BKS;
-    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ln = lane & 15, lg = lane >> 4;
-    const int wr = w >> 2, wc = w & 3;
-
-    const bf16_t* asrc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int p = i * 8 + w, row = 8 * p + (lane >> 3);
-        const int m = min(m0 + row, M - 1);
-        asrc[i] = A + (size_t)m * lda + (((lane & 7) ^ pf_swz<BKS>(row)) << 3);
-    }
-    const bf16_t* bsrc[4];
-    const int ntl = (N + 15) / 16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int b = i * 8 + w, g = n0 / 16 + (b >> 1);
-        const int gg = g < ntl ? g : 0;
-        bsrc[i] = W + ((size_t)gg * (K >> 5) + (b & 1)) * 512 + lane * 8;
-    }
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + w * 1024);
-    auto issue = [&](int kt, int st) {
-        const uint32_t sa = lds0 + st * ST, sb = sa + AST;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pf_glds(asrc[i] + kt * BKS, sa + i * 8192);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pf_glds(bsrc[i] + (size_t)kt * 1024, sb + i * 8192);
-    };
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    issue(0, 0);
-    pf_vm_wait<0>();
-    __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();            // the stagger
-    asm volatile("" ::: "memory");
-    uint4 af[4][2], bf[2][2];                              // this quadrant's A (4 mt) and B (2 nt) fragments
-    for (int kt = 0; kt < nk; ++kt) {
-        const char* sa = smem + (kt & 1) * ST;
-        const char* sb = sa + AST;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int mq = p >> 1, nq = (p == 1 || p == 2) ? 1 : 0;
-            // ---- read section
-            if (p == 0 || p == 2) {
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks)
-                        af[m][ks] = *reinterpret_cast<const uint4*>(
-                            sa + pf_a_off<BKS>(wr * 128 + (mq * 4 + m) * 16 + ln, ks * 4 + lg));
-            }
-            if (p != 2) {
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks)
-                        bf[n][ks] = *reinterpret_cast<const uint4*>(
-                            sb + (((wc * 4 + nq * 2 + n) * 2 + ks) << 10) + lane * 16);
-            }
-            if (p == 0 && kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-            if (p == 3) pf_vm_wait<0>();                   // this wave's copies of step kt + 1
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            // ---- MFMA section
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int n = 0; n < 2; ++n)
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks)
-                        acc[mq * 4 + m][nq * 2 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            as_frag(af[m][ks]), as_frag(bf[n][ks]), acc[mq * 4 + m][nq * 2 + n], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-        }
-    }
-    if (wr == 0) __builtin_amdgcn_s_barrier();            // equal barrier counts
-    pf_epilogue<MODE>(acc, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
-}
-
 }  // namespace
 
 // The prefill regime of zk_gemm_bf16 (split 1, large M): true when the 256 x 256 kernel takes the call.
@@ -342,11 +227,9 @@ int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int 
                const int32_t* skip, void* stream) {
     const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + PF_BN - 1) / PF_BN);
     ZK_REQUIRE(tiles < (1L << 31), "zk_gemm_bf16 (prefill): too many tiles");
-#ifndef ZK_PF_8PH
-#define ZK_PF_8PH 1                // staggered four-phase step (k_gemm_pf8) instead of the one-barrier step
-#endif
+    // (a staggered four-phase form of the step -- two wave groups offset by one barrier, reads of one
+    // overlapping the other's MFMAs -- measured 1-3 % slower: DESIGN.md §6 round 4)
     auto kern = mode == 0 ? &k_gemm_pf<0, PF_BKS, PF_NSTG> : &k_gemm_pf<1, PF_BKS, PF_NSTG>;
-    if (ZK_PF_8PH && PF_BKS == 64) kern = mode == 0 ? &k_gemm_pf8<0> : &k_gemm_pf8<1>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
     hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(PF_NT), PF_LDS, (hipStream_t)stream, (const bf16_t*)A, lda,
                        (const bf16_t*)W, M, N, K, C, (bf16_t*)Cb, skip);

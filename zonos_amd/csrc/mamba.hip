@@ -145,6 +145,20 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
 #ifndef ZK_MB_PD
 #define ZK_MB_PD 1                   // heads' state slices in flight
 #endif
+#ifndef ZK_MB_NT
+#define ZK_MB_NT 0                   // non-temporal SSM state loads / stores under ping-pong
+#endif
+typedef __attribute__((ext_vector_type(4))) unsigned int mb_u32x4;
+__device__ __forceinline__ uint4 mb_ld_state(const bf16_t* p) {
+    if constexpr (ZK_MB_NT & 1)
+        return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const mb_u32x4*>(p)));
+    else return *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ void mb_st_state(bf16_t* p, uint4 v) {
+    if constexpr (ZK_MB_NT & 2)
+        __builtin_nontemporal_store(__builtin_bit_cast(mb_u32x4, v), reinterpret_cast<mb_u32x4*>(p));
+    else *reinterpret_cast<uint4*>(p) = v;
+}
 template <int HP, int DS, int HG, int GS>
 __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
     const float* __restrict__ part, int R, int di, int nh, const float* __restrict__ conv_w,
@@ -212,7 +226,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
     auto load_state = [&](int hh, int buf) {
         const bf16_t* sb = ssr + ((size_t)r * nh + h0 + hh) * HP * DS;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) st[buf][v] = *reinterpret_cast<const uint4*>(sb + st_off(v));
+        for (int v = 0; v < NV; ++v) st[buf][v] = mb_ld_state(sb + st_off(v));
     };
 #pragma unroll
     for (int hh = 0; hh < PD; ++hh) load_state(hh, hh);
@@ -278,7 +292,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
                     a += sn * Cv[e];
                 }
                 accv[v] = a;
-                *reinterpret_cast<uint4*>(ssw + ((size_t)r * nh + h) * HP * DS + st_off(v)) = pack8(svv);
+                mb_st_state(ssw + ((size_t)r * nh + h) * HP * DS + st_off(v), pack8(svv));
             }
             if (hh + PD < HG) load_state(hh + PD, buf);
 #pragma unroll
@@ -311,7 +325,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
                 svv[e] = s;
                 acc += s * s_C[n];
             }
-            *reinterpret_cast<uint4*>(sp + 8 * v) = pack8(svv);
+            mb_st_state(sp + 8 * v, pack8(svv));
         }
         if (hh + PD < HG) load_state(hh + PD, buf);
 #pragma unroll
