@@ -415,7 +415,7 @@ int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const uint16_t* 
  *   x[b][t][c] = v;  s_out[b][t][c] = fp16(Snake_{alpha_next}(v))  (s_f32 = 1: fp32, exact sinf)
  * Replaces the pair zk_dac_conv_cl(k7 -> s2) + zk_dac_conv_cl(1x1, resid = x); the same masking
  * (inputs at t >= lens[b]*scale read 0, outputs there written 0). w7 fp16 [7][C][C], w1 fp16
- * [C][C] (zk_dac_prep_w16 layouts). s_out must not alias s_in. Built for C = 96; the 1x1 sums
+ * [C][C] (zk_dac_prep_w16 layouts). s_out must not alias s_in. Built for C = 96, 192; the 1x1 sums
  * run on 16x16x16 MFMAs (a different fp32 summation grouping than the 32-deep unfused conv:
  * results equal to rounding, not bit for bit). zk_dac_resunit_supported(C): 0 = not fused at this
  * C, 1 = fused except the decode's last unit (the fp32-Snake one), 2 = every unit; zk_dac_decode

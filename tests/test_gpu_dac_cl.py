@@ -112,17 +112,18 @@ def test_conv_cl_vs_torch(Cin, Cout, ks, dil, T, use_resid):
     assert (s32 - s_ref).abs().max().item() < 2e-3 * max(1.0, s_ref.abs().max().item())
 
 
-# the fused residual unit (zk_dac_resunit_cl, C = 96): 512-position tiles, one workgroup per CU;
-# T = 120000 at B = 3 gives 705 tiles, >= 2 per persistent workgroup
-@pytest.mark.parametrize("dil,T", [(1, 300), (3, 517), (9, 1000), (3, 120000)])
-def test_resunit_fused_vs_pair_and_torch(dil, T):
+# the fused residual unit (zk_dac_resunit_cl): C = 96 in 512-position tiles, C = 192 in 256-position
+# tiles, one workgroup per CU; the long cases give >= 2 tiles per persistent workgroup
+@pytest.mark.parametrize("C,dil,T", [(96, 1, 300), (96, 3, 517), (96, 9, 1000), (96, 3, 120000),
+                                     (192, 1, 300), (192, 9, 1000), (192, 3, 70000)])
+def test_resunit_fused_vs_pair_and_torch(C, dil, T):
     L = _lib()
-    C, B, dev = 96, 3, "cuda"
-    assert L.load().zk_dac_resunit_supported(192) == 0      # (96: the product fuses, variants may not)
+    B, dev = 3, "cuda"
+    assert L.load().zk_dac_resunit_supported(384) == 0      # (96 / 192: the product fuses, variants may not)
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    if T >= 100000:
-        assert B * (-(-T // 512)) >= 2 * ncu
-    torch.manual_seed(dil * 1000 + T)
+    if T >= 50000:
+        assert B * (-(-T // (512 if C == 96 else 256))) >= 2 * ncu
+    torch.manual_seed(C + dil * 1000 + T)
     st = L.stream_ptr(torch.device(dev))
     lens = torch.tensor([T, T // 2, 1], dtype=torch.int32, device=dev)
     s_in = torch.randn(B, T, C, device=dev).half()

@@ -132,9 +132,6 @@ constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 #define ZK_CL_SPB 1
 #endif
 constexpr int CL_SPB = ZK_CL_SPB;
-#ifndef ZK_RU_DEPHASE
-#define ZK_RU_DEPHASE 0              // fused unit at OCC 2: the second workgroup round starts this many 10-ns ticks late
-#endif
 // NWM: channel waves (2: the two channel halves; 1: every wave holds all CO_T channels of its
 // positions). FUSE (NWM = 1, one channel tile = all C channels): a whole residual unit in one
 // launch -- the k7 conv's accumulators, Snake'd to fp16, are already the B operands of
@@ -162,7 +159,9 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
     constexpr int NCW = NWM * NWY;               // compute waves
     static_assert(!FUSE || (NWM == 1 && !RES), "fused residual unit: one channel wave, residual in the epilogue");
     constexpr int W1S = CO_T + 8;                // fused: 1x1 weight image row stride (halves)
-    constexpr bool W1LDS = FUSE && OCC == 1;     // fused, one workgroup per CU: 1x1 weights in LDS (else L1)
+    // fused: the 1x1 weights as an LDS image when one workgroup per CU has room for it (C = 96), else
+    // read per output block from L1 / L2, one block ahead
+    constexpr bool W1LDS = FUSE && OCC == 1 && CO_T * W1S * 2 <= 24 * 1024;
     constexpr int QTT = 16 * NQ * NWY;           // positions per tile
     extern __shared__ __attribute__((aligned(16))) char smem[];   // [W ring][X ring][epilogue tables x 2]
 
@@ -206,14 +205,6 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
         g_clprof_rt[blockIdx.x][4] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    if constexpr (FUSE && OCC == 2 && ZK_RU_DEPHASE > 0) {
-        // the second round of workgroups (the one sharing CUs with the first) starts late, so a CU's
-        // two workgroups alternate between the MFMA-bound main loop and the HBM-bound epilogue
-        if (kx >= nper / 2) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ZK_RU_DEPHASE) __builtin_amdgcn_s_sleep(8);
-        }
-    }
     if (wv >= NCW) {
         // ---------------- loader waves: loader lw moves the pieces p with p % NLDK == lw
         // wave-uniform (readfirstlane): the piece counts and the vmcnt switch below stay scalar;
@@ -470,20 +461,33 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
                 }
             };
             load_x(0, 0);
-            // the 1x1 weight fragments are loaded per output block (L1-resident), not hoisted out of
-            // the tile loop into 72 registers held across the main loop
+            // (!W1LDS) the 1x1 weight fragments of output block mo + 1 are loaded while block mo is
+            // multiplied; the opaque pointer keeps hipcc from hoisting all of them out of the tile
+            // loop into registers held across the main loop
             const uint16_t* w1p = w1x1;
             asm volatile("" : "+s"(w1p));
+            uint2 wf[2][W1LDS ? 1 : FM];
+            auto load_w = [&](int mo, int buf) {
+                if constexpr (!W1LDS) {
+#pragma unroll
+                    for (int m = 0; m < FM; ++m)
+                        wf[buf][m] = *reinterpret_cast<const uint2*>(w1p + (mo * 16 + ln) * CO_T + m * 16 + lg * 4);
+                }
+            };
+            load_w(0, 0);
 #pragma unroll
             for (int mo = 0; mo < FM; ++mo) {
-                if (mo + 1 < FM) load_x(mo + 1, (mo + 1) & 1);
+                if (mo + 1 < FM) {
+                    load_w(mo + 1, (mo + 1) & 1);
+                    load_x(mo + 1, (mo + 1) & 1);
+                }
                 f32x4 z[NQ];
 #pragma unroll
                 for (int n = 0; n < NQ; ++n) z[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int m = 0; m < FM; ++m) {
                     const uint2 wa = W1LDS ? *reinterpret_cast<const uint2*>(w1img + (mo * 16 + ln) * W1S + m * 16 + lg * 4)
-                                           : *reinterpret_cast<const uint2*>(w1p + (mo * 16 + ln) * CO_T + m * 16 + lg * 4);
+                                           : wf[mo & 1][W1LDS ? 0 : m];
 #pragma unroll
                     for (int n = 0; n < NQ; ++n)
                         z[n] = __builtin_amdgcn_mfma_f32_16x16x16f16(as_h4(wa), as_h4(h[m][n]), z[n], 0, 0, 0);
@@ -826,27 +830,32 @@ int launch_conv(long ntiles, size_t lds, hipStream_t st, const uint16_t* in, int
     return 0;
 }
 
-// The fused residual unit at C = 96: position waves each holding all 96 channels x 64 positions
-// (FM = 6, NQ = 4), persistent like launch_conv. ZK_RU_OCC 1: one workgroup per CU of 8 position
-// waves (512-position tiles) + 4 loaders, the 1x1 weights in LDS; 2: two workgroups per CU of 4
-// position waves (256 positions) + 2 loaders, the 1x1 weights read through L1 -- one workgroup's
-// HBM-heavy epilogue (x in, x and s out: 10 B per element) then runs beside the other's MFMAs.
+// The fused residual unit: position waves each holding all C channels (C = 96: 64 positions,
+// FM = 6, NQ = 4; C = 192: 32 positions, FM = 12, NQ = 2), persistent like launch_conv. ZK_RU_OCC
+// (C = 96) 1: one workgroup per CU of 8 position waves + 4 loaders, the 1x1 weights in LDS; 2: two
+// workgroups per CU of 4 position waves + 2 loaders, the 1x1 weights read through L1. C = 192: one
+// workgroup per CU of 8 position waves (256-position tiles) + 4 loaders, the 1x1 weights (72 KB)
+// read from L2 one output block ahead.
 #ifndef ZK_RU_OCC
 #define ZK_RU_OCC 1
 #endif
-constexpr int RU_C = 96, RU_FM = 6, RU_NQ = 4, RU_OCC = ZK_RU_OCC, RU_NWY = RU_OCC == 1 ? 8 : 4,
-              RU_NLD = RU_OCC == 1 ? 4 : 2;
-template <bool SF32>
+#ifndef ZK_DAC_FUSE192
+#define ZK_DAC_FUSE192 0             // C = 192 fused: 11.6 ms per unit vs 10.9 for the pair
+#endif
+template <int C_, bool SF32>
 int launch_resunit(const uint16_t* s_in, int B, int T, const uint16_t* w7, const float* b7, int dil, const float* a2,
                    const uint16_t* w1, const float* b1, float* x, const float* alpha_next, void* s_out,
                    const int32_t* lens, int scale, hipStream_t st) {
-    constexpr int NT = 64 * (RU_NWY + RU_NLD);
-    constexpr int qt = 16 * RU_NQ * RU_NWY;
-    auto kern = &k_conv_cl<RU_FM, SF32, false, RU_NQ, CL_DA, RU_OCC, RU_NWY, RU_NLD, CL_SPB, 1, true>;
+    constexpr int FM = C_ / 16, NQ = C_ == 96 ? 4 : 2, OCC = C_ == 96 ? ZK_RU_OCC : 1;
+    constexpr int NWY = OCC == 1 ? 8 : 4, NLD = OCC == 1 ? 4 : 2;
+    constexpr int NT = 64 * (NWY + NLD);
+    constexpr int qt = 16 * NQ * NWY;
+    constexpr bool w1lds = OCC == 1 && C_ * (C_ + 8) * 2 <= 24 * 1024;     // = the kernel's W1LDS
+    auto kern = &k_conv_cl<FM, SF32, false, NQ, CL_DA, OCC, NWY, NLD, CL_SPB, 1, true>;
     const int ks = 7, win = qt + (ks - 1) * dil;
-    const size_t xs = (size_t)((win + 15) / 16) * 1024, ws = (size_t)RU_C * 64;
-    const size_t fixed = (size_t)2 * 6 * RU_C * sizeof(float) + (RU_OCC == 1 ? (size_t)RU_C * (RU_C + 8) * 2 : 0);
-    const size_t cap = RU_OCC == 1 ? 160 * 1024 : 80 * 1024;
+    const size_t xs = (size_t)((win + 15) / 16) * 1024, ws = (size_t)C_ * 64;
+    const size_t fixed = (size_t)2 * 6 * C_ * sizeof(float) + (w1lds ? (size_t)C_ * (C_ + 8) * 2 : 0);
+    const size_t cap = OCC == 1 ? 160 * 1024 : 80 * 1024;
     const int spb = CL_SPB, nws = CL_DA + 2 * spb;
     int dx = std::max(CL_DA, ks), nx = 1 + (dx + 2 * spb - 1 + ks - 1) / ks;
     while (dx > CL_DA && nws * ws + nx * xs + fixed > cap) {
@@ -854,7 +863,7 @@ int launch_resunit(const uint16_t* s_in, int B, int T, const uint16_t* w7, const
         nx = 1 + (dx + 2 * spb - 1 + ks - 1) / ks;
     }
     const size_t lds = nws * ws + nx * xs + fixed;
-    ZK_REQUIRE(lds <= cap, "zk_dac_resunit_cl: LDS %zu too large (dil %d)", lds, dil);
+    ZK_REQUIRE(lds <= cap, "zk_dac_resunit_cl: LDS %zu too large (C %d dil %d)", lds, C_, dil);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     int dev = 0, ncu = 0, occ = 0;
     ZK_HIP(hipGetDevice(&dev));
@@ -866,7 +875,7 @@ int launch_resunit(const uint16_t* s_in, int B, int T, const uint16_t* w7, const
     ZK_REQUIRE(ntiles < (1L << 31), "zk_dac_resunit_cl: too many tiles");
     const long resident = (long)ncu * occ / 8 * 8;
     const long grid = std::min<long>((ntiles + 7) / 8 * 8, std::max<long>(resident, 8));
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, s_in, RU_C, T, w7, 0L, b7, RU_C, ks, dil,
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, s_in, C_, T, w7, 0L, b7, C_, ks, dil,
                        3 * dil, T, 1, 1, 0, T, x, x, a2, s_out, (int)SF32, lens, scale, scale, nq, nx, dx, B, w1, b1,
                        alpha_next);
     return 0;
@@ -989,13 +998,15 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
 #ifndef ZK_DAC_FUSE
 #define ZK_DAC_FUSE 1
 #endif
-extern "C" int zk_dac_resunit_supported(int C) { return C == RU_C ? ZK_DAC_FUSE : 0; }
+extern "C" int zk_dac_resunit_supported(int C) {
+    return C == 96 ? ZK_DAC_FUSE : (C == 192 && ZK_DAC_FUSE192 ? ZK_DAC_FUSE : 0);
+}
 
 extern "C" int zk_dac_resunit_cl(const uint16_t* s_in, int B, int C, int T, const uint16_t* w7, const float* b7,
                                  int dil, const float* a2, const uint16_t* w1, const float* b1, float* x,
                                  const float* alpha_next, void* s_out, int s_f32, const int32_t* lens, int scale,
                                  void* stream) {
-    ZK_REQUIRE(C == RU_C, "zk_dac_resunit_cl: C=%d (the fused unit is built for C = %d)", C, RU_C);
+    ZK_REQUIRE(C == 96 || C == 192, "zk_dac_resunit_cl: C=%d (the fused unit is built for C = 96 and 192)", C);
     ZK_REQUIRE(dil >= 1 && 6 * dil <= MAXSPAN, "zk_dac_resunit_cl: dil=%d", dil);
     ZK_REQUIRE(s_in != nullptr && w7 && b7 && a2 && w1 && b1 && x && alpha_next && s_out,
                "zk_dac_resunit_cl: null argument");
@@ -1003,8 +1014,10 @@ extern "C" int zk_dac_resunit_cl(const uint16_t* s_in, int B, int C, int T, cons
                "zk_dac_resunit_cl: s_out must not alias s_in (neighbouring tiles read it as their halo)");
     if (B == 0 || T <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (s_f32) ZK_TRY(launch_resunit<true>(s_in, B, T, w7, b7, dil, a2, w1, b1, x, alpha_next, s_out, lens, scale, st));
-    else ZK_TRY(launch_resunit<false>(s_in, B, T, w7, b7, dil, a2, w1, b1, x, alpha_next, s_out, lens, scale, st));
+#define ZK_RU(C_, F_) ZK_TRY((launch_resunit<C_, F_>(s_in, B, T, w7, b7, dil, a2, w1, b1, x, alpha_next, s_out, lens, scale, st)))
+    if (C == 96) { if (s_f32) ZK_RU(96, true); else ZK_RU(96, false); }
+    else { if (s_f32) ZK_RU(192, true); else ZK_RU(192, false); }
+#undef ZK_RU
     ZK_CHECK_LAUNCH("zk_dac_resunit_cl");
     return 0;
 }
