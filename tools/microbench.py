@@ -252,7 +252,7 @@ def mamba():
              ptr(posd), ptr(ssms[i][0]), ptr(ssms[i][1]), ptr(A), ptr(dtb), ptr(Dv), ptr(yz), None, S)
     us = timeit(f, reps=40, warm=8)
     b = R * di * ds * 2 * 2 + R * conv_dim * 8 * 2 + gs * R * ncol * 4 + R * di * 4
-    print(f"mamba_step R={R} grouped={os.environ.get('ZK_MAMBA_GROUPED', '1')}: {us:7.2f} us  "
+    print(f"mamba_step R={R}: {us:7.2f} us  "
           f"{b / 1e6:6.1f} MB  {b / (us * 1e-6) / 1e9:6.0f} GB/s", flush=True)
 
 
