@@ -132,9 +132,6 @@ constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 #define ZK_CL_SPB 1
 #endif
 constexpr int CL_SPB = ZK_CL_SPB;
-#ifndef ZK_RU_DEPHASE
-#define ZK_RU_DEPHASE 0              // fused unit: odd workgroups start this many 10-ns ticks late
-#endif
 // NWM: channel waves (2: the two channel halves; 1: every wave holds all CO_T channels of its
 // positions). FUSE (NWM = 1, one channel tile = all C channels): a whole residual unit in one
 // launch -- the k7 conv's accumulators, Snake'd to fp16, are already the B operands of
@@ -208,14 +205,6 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
         g_clprof_rt[blockIdx.x][4] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    if constexpr (FUSE && ZK_RU_DEPHASE > 0) {
-        // half the workgroups start late, so at any time about half the CUs run the MFMA-bound main
-        // loop while the others run the HBM-bound epilogue
-        if (kx & 1) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ZK_RU_DEPHASE) __builtin_amdgcn_s_sleep(8);
-        }
-    }
     if (wv >= NCW) {
         // ---------------- loader waves: loader lw moves the pieces p with p % NLDK == lw
         // wave-uniform (readfirstlane): the piece counts and the vmcnt switch below stay scalar;
@@ -952,10 +941,7 @@ extern "C" int zk_dac_conv_cl(const uint16_t* in, int B, int Cin, int Tin, const
 #ifndef ZK_CL_WIDE
 #define ZK_CL_WIDE 1
 #endif
-#ifndef ZK_CL_WIDE_CT
-#define ZK_CL_WIDE_CT 0
-#endif
-    const bool wide = ZK_CL_WIDE && resid == nullptr && !s_f32 && (nphase == 1 || ZK_CL_WIDE_CT) && FM <= 3;
+    const bool wide = ZK_CL_WIDE && resid == nullptr && !s_f32 && nphase == 1 && FM <= 3;
     // fat: the wide convs as ONE workgroup per CU of 8 compute waves (2 channel halves x 4 position
     // quarters, 512-position tiles) + 4 loaders = 12 waves, exactly 3 per SIMD. Two 6-wave
     // workgroups per CU (the same compute per step) were co-resident only where the wave placement

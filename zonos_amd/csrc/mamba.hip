@@ -146,7 +146,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
 #define ZK_MB_PD 1                   // heads' state slices in flight
 #endif
 #ifndef ZK_MB_NT
-#define ZK_MB_NT 3                   // non-temporal SSM state loads (1) / stores (2): c5 decode 4.42 -> 4.34 ms
+#define ZK_MB_NT 3                   // non-temporal SSM state loads (1) / stores (2): c5 decode 4.42 -> 4.34 ms (the stores; loads alone 4.47-4.49)
 #endif
 typedef __attribute__((ext_vector_type(4))) unsigned int mb_u32x4;
 __device__ __forceinline__ uint4 mb_ld_state(const bf16_t* p) {
