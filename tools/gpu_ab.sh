@@ -12,7 +12,11 @@
 #                         zonos_amd.build.build_variant), twice, interleaved
 #   benchv:NAME[:ARGS]    bench.py ARGS on the product library and every variant, twice,
 #                         interleaved -> OUT/benchv_NAME.log (value + decode ms per step)
+#   testsv:PYTEST_K       pytest -m gpu -k PYTEST_K on every variant (parity must hold for any tuning)
 #   prof:NAME[:ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> OUT/prof_NAME/*stats.csv
+#   pmcstd:ROUND          HBM bytes per launch of the decode attention (c3 shape, tools/attn_pmc.py) and
+#                         the hybrid SSM step (c5 shape, microbench mamba): FETCH_SIZE / WRITE_SIZE in
+#                         separate passes -> OUT/ROUND_{attn_fused,mamba_step}_pmc.{json,txt}
 #   pmc:NAME:COUNTERS[:ARGS]  one rocprofv3 --pmc pass (COUNTERS comma-separated, within one
 #                         block's limits) of bench.py ARGS -> OUT/pmc_NAME/
 set -e
@@ -51,6 +55,25 @@ for step in "$@"; do
       done > "$OUT/benchv_$name.log" 2>&1
       rm -f "$OUT/benchv_tmp.log"
       cat "$OUT/benchv_$name.log" ;;
+    testsv)
+      for v in $(ls zonos_amd/lib/variants 2>/dev/null); do
+        ZK_LIB_PATH=zonos_amd/lib/variants/$v/libzonos_hip.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+            --timeout 300 --timeout-method thread -k "$rest" > "$OUT/tests_$v.log" 2>&1
+        echo "$v: $(tail -n 1 "$OUT/tests_$v.log")"
+      done ;;
+    pmcstd)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d "$OUT/attn_$c" -o run --output-format csv -- \
+            python3 tools/attn_pmc.py > "$OUT/attn_$c.log" 2>&1
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d "$OUT/mamba_$c" -o run --output-format csv -- \
+            python3 tools/microbench.py mamba > "$OUT/mamba_$c.log" 2>&1
+      done
+      python tools/pmc_summary.py "$OUT/attn_FETCH_SIZE" "$OUT/attn_WRITE_SIZE" --match "k_attn_decode<true" --R 128 \
+          --ctx 1705 --alg 454033408 --json "$OUT/${rest}_attn_fused_pmc.json" > "$OUT/${rest}_attn_fused_pmc.txt"
+      python tools/pmc_summary.py "$OUT/mamba_FETCH_SIZE" "$OUT/mamba_WRITE_SIZE" --match "k_mamba_step" --R 128 \
+          --ctx 0 --alg 288161792 --json "$OUT/${rest}_mamba_step_pmc.json" > "$OUT/${rest}_mamba_step_pmc.txt"
+      find "$OUT" -name "*.csv" -path "*_SIZE*" -delete
+      cat "$OUT/${rest}_attn_fused_pmc.json" "$OUT/${rest}_mamba_step_pmc.json" ;;
     prof)
       name=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
