@@ -278,6 +278,44 @@ def make_copy_fixtures():
         np.savez_compressed(os.path.join(HERE, f"gen_{name}.npz"), **d)
 
 
+# Edge shapes of generate() (model.py:264-301 sizes every buffer from P and max_new_tokens): no audio
+# prefix, one new token, fewer new tokens than codebooks (the delay pattern's diagonal never
+# completes), exactly 9 / 10, odd batch sizes. Copy heads, greedy: every decision has a wide margin.
+EDGE_CASES = [  # (B, P, max_new, Lc)
+    (1, 0, 1, 5), (1, 0, 9, 8), (2, 4, 2, 12), (3, 1, 10, 7), (2, 0, 17, 3), (1, 6, 5, 12),
+]
+
+
+def make_edge_fixtures():
+    from tests.golden_util import COPY
+    sp = GEN_CASES["greedy"]["sp"]
+    W = zonos_ref.make_copy_weights(COPY, seed=0, copy_gain=COPY_GAIN)
+    model = build_ref_model(COPY, W)
+    d = dict(wsum=np.array(wsum(W)), copy_gain=np.float32(COPY_GAIN), n=np.int32(len(EDGE_CASES)))
+    for i, (B, P, max_new, Lc) in enumerate(EDGE_CASES):
+        cond = zonos_ref.synthetic_conditioning(B, Lc, COPY.d_model, seed=10 + i)
+        prefix = zonos_ref.synthetic_prefix_codes(B, P, seed=20 + i) if P else None
+        seed = 77 + i
+        out, _ = run_generate(model, cond, prefix, B, max_new, sp, seed, 0)
+        trace = {}
+        out_o = zonos_ref.generate(zonos_ref.pad_heads(W, COPY), COPY, cond, prefix, max_new, 2.0, B, sp,
+                                   seed=seed, trace=trace)
+        same = len(out) == len(out_o) and all(torch.equal(a, b) for a, b in zip(out, out_o))
+        m = decision_margins(trace)
+        codes, lens = pack_codes(out)
+        print(f"[gen:edge{i}] B={B} P={P} new={max_new} lens={lens.tolist()} oracle_match={same} "
+              f"min margin {m.min():.3f}")
+        assert same, f"oracle diverges from reference on edge case {i}"
+        d.update({f"e{i}_shape": np.array([B, P, max_new, Lc, seed], dtype=np.int64),
+                  f"e{i}_cond": cond.view(torch.int16).numpy(), f"e{i}_codes": codes, f"e{i}_lens": lens,
+                  f"e{i}_margins": m.astype(np.float32), f"e{i}_delayed": trace["delayed"].numpy().astype(np.int16)})
+        if P:
+            d[f"e{i}_prefix"] = prefix.numpy().astype(np.int16)
+    for k, v in sp.items():
+        d["sp_" + k] = np.float64(v)
+    np.savez_compressed(os.path.join(HERE, "gen_edge.npz"), **d)
+
+
 def ref_forced_steps(model, cond, delayed, P, windows, sp, seed, row_base):
     """The reference's own prefill (model.py:181-202) over a forced history, then its single-token
     decode (model.py:118-142), its logit bias (332-334, EOS never accepted: benchmark mode) and
@@ -580,6 +618,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "copy":
         make_copy_fixtures()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "edge":
+        make_edge_fixtures()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "full":
         make_full_fixtures(tuple(sys.argv[2:]) or ("c1", "c2", "c3"))
         sys.exit(0)
@@ -587,6 +628,7 @@ if __name__ == "__main__":
     make_sampler_fixtures()
     make_generate_fixtures()
     make_copy_fixtures()
+    make_edge_fixtures()
     make_full_fixtures()
     make_dac_fixtures()
     make_dac_long_fixture()

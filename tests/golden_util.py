@@ -131,6 +131,28 @@ def load_gen_case(name):
                 margins=d["margins"] if "margins" in d.files else None)
 
 
+def load_edge_cases():
+    """gen_edge.npz (make_golden.make_edge_fixtures): generate() at edge shapes on copy heads --
+    no audio prefix, 1 / 2 / 5 / 9 / 10 / 17 new tokens, B = 1, 2, 3. Returns (W_raw, W, wsum, sp, cases)."""
+    d = np.load(os.path.join(G, "gen_edge.npz"))
+    sp = {k[3:]: float(d[k]) for k in d.files if k.startswith("sp_")}
+    sp["top_k"] = int(sp["top_k"])
+    sp["repetition_penalty_window"] = int(sp["repetition_penalty_window"])
+    W_raw = zonos_ref.make_copy_weights(COPY, seed=0, copy_gain=float(d["copy_gain"]))
+    cases = []
+    for i in range(int(d["n"])):
+        B, P, max_new, Lc, seed = (int(v) for v in d[f"e{i}_shape"])
+        cases.append(dict(B=B, P=P, max_new=max_new, Lc=Lc, seed=seed,
+                          cond=torch.from_numpy(d[f"e{i}_cond"]).view(torch.bfloat16),
+                          prefix=torch.from_numpy(d[f"e{i}_prefix"].astype(np.int64)) if P else None,
+                          codes=d[f"e{i}_codes"], lens=d[f"e{i}_lens"], margins=d[f"e{i}_margins"],
+                          delayed=d[f"e{i}_delayed"]))
+    return W_raw, zonos_ref.pad_heads(W_raw, COPY), str(d["wsum"]), sp, cases
+
+
+EDGE_N = 6
+
+
 # ---- PrefixConditioner fixtures (cond.npz; made by make_golden.make_cond_fixtures)
 COND_PHONEMES = {"hello": "həlˈoʊ wˈɜːld!", "long": "ðɪs ɪz ə lˈɔŋɡɚ sˈɛntəns, wɪð pˈʌŋktʃuːˈeɪʃən… ænd ɐ ʔ",
                  "unk": "a1b"}

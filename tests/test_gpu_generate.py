@@ -6,7 +6,7 @@ import torch
 
 from oracle import zonos_ref
 
-from .golden_util import COPY_CASES, GEN_CASES, TINY, load_gen_case
+from .golden_util import COPY, COPY_CASES, EDGE_N, GEN_CASES, TINY, load_edge_cases, load_gen_case
 
 pytestmark = pytest.mark.gpu
 
@@ -50,6 +50,33 @@ def test_free_running_greedy_bit_identical(name, graph):
     assert lens == c["lens"].tolist()
     for i, x in enumerate(out):
         assert np.array_equal(x.cpu().numpy(), c["codes"][i, :, :lens[i]]), i
+
+
+@pytest.mark.parametrize("i", range(EDGE_N))
+@pytest.mark.parametrize("graph", [True, False])
+def test_free_running_edge_shapes_bit_identical(i, graph):
+    """generate() at its edge shapes (gen_edge.npz, reference-generated): no audio prefix, one new
+    token, fewer new tokens than codebooks (the delay diagonal never completes), exactly 9 / 10 / 17,
+    B = 1, 2, 3 -- codes and output lengths bit for bit, graph and eager."""
+    W_raw, W, ws, sp, cases = _edge()
+    c = cases[i]
+    assert c["margins"].min() > 2.0
+    eng = _engine(W, COPY)
+    prefix = c["prefix"].cuda() if c["prefix"] is not None else None
+    out = eng.generate(c["cond"].cuda(), prefix, c["max_new"], 2.0, c["B"], sp, seed=c["seed"], use_graph=graph,
+                       poll_every=3)
+    assert [int(x.shape[1]) for x in out] == c["lens"].tolist()
+    for b, x in enumerate(out):
+        assert np.array_equal(x.cpu().numpy(), c["codes"][b, :, :c["lens"][b]]), b
+
+
+_EDGE = []
+
+
+def _edge():
+    if not _EDGE:
+        _EDGE.append(load_edge_cases())
+    return _EDGE[0]
 
 
 def _margins(decision):

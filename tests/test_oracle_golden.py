@@ -10,8 +10,8 @@ import torch
 from oracle import dac_ref, zonos_ref
 from oracle.philox import exp_noise, philox4x32_10
 
-from .golden_util import (CLI_SP, COND_CASES, COPY_CASES, ENC_DAC, FULL, FULL_SEED, GEN_CASES, GREEDY_SP, TINY_DAC,
-                          cond_case, full_weights, load_enc_case, load_full_case, load_gen_case, wsum)
+from .golden_util import (CLI_SP, COND_CASES, COPY, COPY_CASES, ENC_DAC, FULL, FULL_SEED, GEN_CASES, GREEDY_SP, TINY_DAC,
+                          cond_case, full_weights, load_edge_cases, load_enc_case, load_full_case, load_gen_case, wsum)
 
 G = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -70,6 +70,21 @@ def test_generate_golden(name):
     if c["logits"] is not None:
         got = torch.stack(trace["logits"][:len(c["logits"])]).numpy()
         assert np.array_equal(got, c["logits"])
+
+
+def test_generate_edge_shapes_golden():
+    """The restatement at generate()'s edge shapes (no prefix, 1 new token, fewer new tokens than
+    codebooks, odd batches) reproduces the reference's codes and delayed buffer."""
+    W_raw, W, ws, sp, cases = load_edge_cases()
+    assert wsum(W_raw) == ws
+    for i, c in enumerate(cases):
+        trace = {}
+        out = zonos_ref.generate(W, COPY, c["cond"], c["prefix"], c["max_new"], 2.0, c["B"], sp, seed=c["seed"],
+                                 trace=trace)
+        assert [int(x.shape[1]) for x in out] == c["lens"].tolist(), i
+        for b, x in enumerate(out):
+            assert np.array_equal(x.numpy(), c["codes"][b, :, :c["lens"][b]]), (i, b)
+        assert np.array_equal(trace["delayed"].numpy(), c["delayed"]), i
 
 
 @pytest.mark.parametrize("name", ["dac_tiny", "dac_44k"])
