@@ -80,6 +80,8 @@ def test_delay_pattern_golden():
                                           # decode shapes (k_gemm_ws / k_gemv_rk)
                                           (128, 2048, 2048, 8), (128, 9234, 2048, 2), (128, 16384, 2048, 1),
                                           (128, 2048, 2048, 4), (100, 2048, 8192, 4), (1, 3072, 2048, 2),
+                                          # < 192 tiles of 64 columns: 32-column workgroups (c5 Mamba in_proj)
+                                          (128, 8512, 2048, 1), (72, 3000, 512, 1),
                                           # prefill shapes (k_gemm, M >= 1024)
                                           (1100, 256, 512, 1), (2048, 384, 2048, 1), (1024, 1152, 128, 1),
                                           # prefill shapes with >= 256 tiles of 256 x 256 (k_gemm_pf): ragged
@@ -98,6 +100,25 @@ def test_gemm_vs_fp32(M, N, K, nsplit):
     ref = A.float() @ W.float().t()
     # fp32 accumulation of bf16 products: error ~ K * eps32 * |a||w|
     assert torch.allclose(got, ref, atol=2e-3 * (K / 2048) ** 0.5, rtol=1e-3), (got - ref).abs().max()
+
+
+def test_gemm_narrow_workgroups_bit_identical():
+    """The 32-column k_gemm_ws workgroups (slab GEMMs with < 192 64-column tiles, e.g. the c5 Mamba
+    in_proj N = 8512) keep each column's K order: columns equal, bit for bit, those of the 64-column
+    form (forced by appending columns until the grid has 192 tiles)."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import pack_weights
+    M, N, K, N2 = 128, 8512, 2048, 12288
+    g = torch.Generator(device="cpu").manual_seed(7)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    W2 = (torch.randn(N2, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    outs = []
+    for n in (N, N2):
+        Wpk = pack_weights(W2[:n].contiguous(), stream_ptr())
+        part = torch.empty(1, M, n, device=DEV)
+        call("zk_gemm_bf16", ptr(A), K, ptr(Wpk), M, n, K, 1, 0, ptr(part), None, None, stream_ptr())
+        outs.append(part[0, :, :N])
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_pack_weights_layout():

@@ -87,13 +87,16 @@ ZK_DEV void ws_tile(int L, int gx, int gz, int& bx, int& bz) {
 // Returns the number of loads issued (2 per chunk).
 // `chunks` packs the GEMM's column groups per compute wave (k_gemm_ws NG) in bits 8+: wave w of
 // workgroup (bx, bz) streams the 16-row tiles (bx * 4 + w) * NG + g, g < NG.
+// chunks: bits 0-7 chunks per wave, 8-15 column groups per wave (NG, 0 = 1), 16-23 compute waves per
+// workgroup of the warmed GEMM (0 = 4)
+ZK_DEV int warm_nw(int chunks) { return (chunks >> 16) ? (chunks >> 16) : 4; }
 ZK_DEV int warm_unit(const bf16_t* W, int K, int gx, int gz, int chunks, int L, int w, int lane, void* sink) {
     int bx, bz;
     ws_tile(L, gx, gz, bx, bz);
-    const int ng = max(1, chunks >> 8), nch = chunks & 255;
+    const int ng = max(1, (chunks >> 8) & 255), nch = chunks & 255, nw = warm_nw(chunks);
     const int kbeg = bz * (K / gz);
     for (int g = 0; g < ng; ++g) {
-        const bf16_t* p = W + ((size_t)((bx * 4 + w) * ng + g) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
+        const bf16_t* p = W + ((size_t)((bx * nw + w) * ng + g) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
         for (int c = 0; c < nch; ++c) {
             __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024), sink, 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024 + 512), sink, 16, 0, 0);
@@ -107,10 +110,11 @@ ZK_DEV int warm_unit(const bf16_t* W, int K, int gx, int gz, int chunks, int L, 
 // taking units first, first + step, ...
 ZK_DEV void warm_units(const bf16_t* W, int K, int gx, int gz, int chunks, int r, int nwg, int first, int step,
                        int lane, void* sink) {
+    const int nw = warm_nw(chunks);
     for (int u = first;; u += step) {
-        const int L = r + (u >> 2) * nwg;
+        const int L = r + (u / nw) * nwg;
         if (L >= gx * gz) break;
-        warm_unit(W, K, gx, gz, chunks, L, u & 3, lane, sink);
+        warm_unit(W, K, gx, gz, chunks, L, u % nw, lane, sink);
     }
 }
 

@@ -452,11 +452,12 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
             float* C = Cpart + (size_t)split * M * N;
             constexpr int LPR = BNW / 4;                         // lanes per row (4 floats each)
             constexpr int RPI = 64 / LPR;                        // whole rows per instruction
+            constexpr int NQI = (MT * 16 + RPI - 1) / RPI;       // (BNW = 48: 5 rows per instruction, 4 lanes idle)
             const int c4 = (lane % LPR) * 4;
 #pragma unroll
-            for (int q = w; q < MT * 16 / RPI; q += NCW) {
+            for (int q = w; q < NQI; q += NCW) {
                 const int m = q * RPI + lane / LPR;
-                if (m < M && n0 + c4 < N) {
+                if (lane < RPI * LPR && m < M && n0 + c4 < N) {
                     const f32x4 v = *reinterpret_cast<const f32x4*>(tile + m * TS + c4);
                     float* dst = C + (size_t)m * N + n0 + c4;
                     if (n0 + c4 + 3 < N) {
@@ -473,11 +474,12 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
             const int F = N / 2;
             constexpr int GPR = BNW / 16;                        // 16-column groups per row
             constexpr int RPI = 64 / GPR;                        // rows per instruction
+            constexpr int NQI = (MT * 16 + RPI - 1) / RPI;
             const int f0 = n0 / 2, gi = lane % GPR;              // group gi -> outputs f0 + 8 gi ..
 #pragma unroll
-            for (int q = w; q < MT * 16 / RPI; q += NCW) {
+            for (int q = w; q < NQI; q += NCW) {
                 const int m = q * RPI + lane / GPR;
-                if (m < M && f0 + gi * 8 < F) {
+                if (lane < RPI * GPR && m < M && f0 + gi * 8 < F) {
                     const float* yv = tile + m * TS + gi * 16;
                     float o[8];
 #pragma unroll
@@ -968,6 +970,13 @@ extern "C" int zk_pack_weights(const void* w, int N, int K, void* out, void* str
 #ifndef ZK_WS_NCW
 #define ZK_WS_NCW 4                // k_gemm_ws compute waves (16-column tiles) per workgroup
 #endif
+#ifndef ZK_WS_NARROW
+#define ZK_WS_NARROW 3             // compute waves of the narrow workgroups for slab GEMMs with < 192 64-column tiles (0: off)
+#endif
+#define ZK_WS_NARROW_W (ZK_WS_NARROW > 0 ? ZK_WS_NARROW : 1)
+#ifndef ZK_WS_NARROW_BELOW
+#define ZK_WS_NARROW_BELOW 192     // ... when the 64-column grid has fewer workgroups than this
+#endif
 
 // k_gemm_ws regime of zk_gemm_bf16_warm below (16 < M <= 128 or M <= 16 with K/nsplit % 128 != 0)
 static bool ws_regime(int M, int K, int nsplit) {
@@ -998,11 +1007,20 @@ bool zk_gemm_pf_applies(int M, int N, int K, int nsplit);
 int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int mode, float* C, void* Cb,
                const int32_t* skip, void* stream);
 
+// the narrow k_gemm_ws form (ZK_WS_NARROW compute waves per workgroup) for this slab GEMM?
+static bool ws_narrow(int M, int N, int nsplit, int mode, int ng) {
+    if (ZK_WS_NARROW <= 0 || ZK_WS_NCW != 4 || mode != 0 || M <= 64 || ng != 1) return false;
+    const long nnar = (long)(N + 16 * ZK_WS_NARROW - 1) / (16 * ZK_WS_NARROW) * nsplit;
+    return (long)((N + 63) / 64) * nsplit < ZK_WS_NARROW_BELOW && nnar <= 256;
+}
+
 ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int mode, int chunks) {
     if (W == nullptr || M <= 16 || ZK_WS_NCW != 4 || !ws_regime(M, K, nsplit) || K % (nsplit * BK) != 0)
         return ZkWarm{nullptr, 0, 0, 0, 0};
     const int ng = ws_ng(N, mode);
-    return ZkWarm{W, K, (N + BN * ng - 1) / (BN * ng), nsplit, std::min(chunks, K / nsplit / BK) | (ng > 1 ? ng << 8 : 0)};
+    const int nw = ws_narrow(M, N, nsplit, mode, ng) ? ZK_WS_NARROW : 4;
+    return ZkWarm{W, K, (N + 16 * nw * ng - 1) / (16 * nw * ng), nsplit,
+                  std::min(chunks, K / nsplit / BK) | (ng > 1 ? ng << 8 : 0) | (nw != 4 ? nw << 16 : 0)};
 }
 
 extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
@@ -1057,24 +1075,33 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
     if (M <= BM && nchunks <= 32) {
         constexpr int NCW = ZK_WS_NCW;            // compute waves per workgroup
         const int ng = M > 16 && NCW == 4 ? ws_ng(N, mode) : 1;
-        dim3 g((N + 16 * NCW * ng - 1) / (16 * NCW * ng), 1, nsplit);
+        // a slab GEMM whose 64-column tiles x splits leave a quarter of the CUs idle (the c5 Mamba
+        // in_proj: N = 8512 unsplit, 133 tiles) runs narrower workgroups of ZK_WS_NARROW compute
+        // waves (16 columns each) while the grid still fits one workgroup per CU; the same
+        // per-column K order (bit-identical results). (32 columns = 266 workgroups for 256 CUs:
+        // c5 decode 4.34 -> 4.64 ms.)
+        const bool narrow = ws_narrow(M, N, nsplit, mode, ng);
+        const int ncw = narrow ? ZK_WS_NARROW : NCW;
+        dim3 g((N + 16 * ncw * ng - 1) / (16 * ncw * ng), 1, nsplit);
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
         const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2 + (warm.W ? 1024 : 0);     // + warm-up sink
-#define ZK_WS_LAUNCH4(MODE_, NCH_, MT_, NG_)                                                                       \
+#define ZK_WS_LAUNCH5(MODE_, NCH_, MT_, NG_, NCW_)                                                                 \
     do {                                                                                                          \
-        constexpr int NB_ = NG_ > 1 ? ZK_WS_NGNB : (NCW > 4 ? 1 : 2);                                             \
-        auto kern_ = &k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW, NG_, NB_>;                        \
+        constexpr int NB_ = NG_ > 1 ? ZK_WS_NGNB : (NCW_ > 4 ? 1 : 2);                                            \
+        auto kern_ = &k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW_, NG_, NB_>;                       \
         if (lds > 65536)                                                                                          \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern_), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)lds);                                                                        \
-        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW + WS_NLD)), lds, (hipStream_t)stream,                         \
+        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW_ + WS_NLD)), lds, (hipStream_t)stream,                        \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
                            skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks);              \
         handled = true;                                                                                           \
     } while (0)
+#define ZK_WS_LAUNCH4(MODE_, NCH_, MT_, NG_) ZK_WS_LAUNCH5(MODE_, NCH_, MT_, NG_, NCW)
 #define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
     do {                                                                                                          \
         if ((MT_) == 8 && ng == 2) ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 2);                                            \
+        else if ((MODE_) == 0 && (MT_) == 8 && narrow) ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, ZK_WS_NARROW_W);          \
         else ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 1);                                                                  \
     } while (0)
 #define ZK_WS_LAUNCH(MODE_, NCH_)                                                                                  \
@@ -1109,6 +1136,7 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
             ZK_CHECK_LAUNCH("zk_gemm_bf16");
             return 0;
         }
+#undef ZK_WS_LAUNCH5
 #undef ZK_WS_LAUNCH4
 #undef ZK_WS_LAUNCH3
 #undef ZK_WS_LAUNCH
