@@ -132,6 +132,9 @@ constexpr int CL_THREADS = 256 + 64 * CL_NLD;   // 4 compute waves + the loaders
 #define ZK_CL_SPB 1
 #endif
 constexpr int CL_SPB = ZK_CL_SPB;
+#ifndef ZK_RU_XPD
+#define ZK_RU_XPD 4                  // fused unit: residual output blocks in flight in the epilogue
+#endif
 // NWM: channel waves (2: the two channel halves; 1: every wave holds all CO_T channels of its
 // positions). FUSE (NWM = 1, one channel tile = all C channels): a whole residual unit in one
 // launch -- the k7 conv's accumulators, Snake'd to fp16, are already the B operands of
@@ -451,7 +454,10 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
             }
             // residual rows of output block mo (clamped loads; out-of-range positions are not stored),
             // one block ahead of the block being multiplied
-            float4 xr[2][NQ];
+            // (XPD output blocks of residual rows in flight: the accumulators are packed into h by now,
+            // so their registers hold the prefetch)
+            constexpr int XPD = ZK_RU_XPD < FM ? ZK_RU_XPD : FM;
+            float4 xr[XPD][NQ];
             auto load_x = [&](int mo, int buf) {
 #pragma unroll
                 for (int n = 0; n < NQ; ++n) {
@@ -460,7 +466,8 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
                     xr[buf][n] = *reinterpret_cast<const float4*>(resid + ((size_t)b * Tout + tt) * Cout + mo * 16 + lg * 4);
                 }
             };
-            load_x(0, 0);
+#pragma unroll
+            for (int p = 0; p < XPD; ++p) load_x(p, p);
             // (!W1LDS) the 1x1 weight fragments of output block mo + 1 are loaded while block mo is
             // multiplied; the opaque pointer keeps hipcc from hoisting all of them out of the tile
             // loop into registers held across the main loop
@@ -477,10 +484,7 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
             load_w(0, 0);
 #pragma unroll
             for (int mo = 0; mo < FM; ++mo) {
-                if (mo + 1 < FM) {
-                    load_w(mo + 1, (mo + 1) & 1);
-                    load_x(mo + 1, (mo + 1) & 1);
-                }
+                if (mo + 1 < FM) load_w(mo + 1, (mo + 1) & 1);
                 f32x4 z[NQ];
 #pragma unroll
                 for (int n = 0; n < NQ; ++n) z[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -504,7 +508,7 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
                     const size_t o = ((size_t)b * Tout + tt) * Cout + co;
                     float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
                     if (tt < len_out) {
-                        const float4 r = xr[mo & 1][n];
+                        const float4 r = xr[mo % XPD][n];
                         v0 = __fadd_rn(r.x, __fadd_rn(z[n][0], bb.x));
                         v1 = __fadd_rn(r.y, __fadd_rn(z[n][1], bb.y));
                         v2 = __fadd_rn(r.z, __fadd_rn(z[n][2], bb.z));
@@ -519,6 +523,7 @@ __global__ __launch_bounds__(64 * (NWM * NWY + NLDK), ZK_CL_LBW(OCC, 64 * (NWM *
                             pack_h4(snake_fast(v0, aa.x, rr.x), snake_fast(v1, aa.y, rr.y),
                                     snake_fast(v2, aa.z, rr.z), snake_fast(v3, aa.w, rr.w));
                 }
+                if (mo + XPD < FM) load_x(mo + XPD, mo % XPD);       // into the slot just consumed
             }
             continue;
         }
