@@ -102,22 +102,24 @@ def test_gemm_vs_fp32(M, N, K, nsplit):
     assert torch.allclose(got, ref, atol=2e-3 * (K / 2048) ** 0.5, rtol=1e-3), (got - ref).abs().max()
 
 
-def test_gemm_narrow_workgroups_bit_identical():
-    """The 32-column k_gemm_ws workgroups (slab GEMMs with < 192 64-column tiles, e.g. the c5 Mamba
-    in_proj N = 8512) keep each column's K order: columns equal, bit for bit, those of the 64-column
-    form (forced by appending columns until the grid has 192 tiles)."""
+@pytest.mark.parametrize("N,N2,nsplit", [(8512, 12288, 1), (9234, 10304, 2)])
+def test_gemm_narrow_wide_workgroups_bit_identical(N, N2, nsplit):
+    """k_gemm_ws workgroups of 3 waves (48 columns: slab GEMMs with < 192 64-column tiles, the c5 Mamba
+    in_proj N = 8512) and of 5 waves (80 columns: > 256 tiles, the heads GEMM N = 9234 split 2) keep
+    each column's K order: every split's columns equal, bit for bit, those of the 64-column form
+    (forced by appending columns until neither grid rule applies)."""
     from zonos_amd._lib import call, ptr, stream_ptr
     from zonos_amd.engine import pack_weights
-    M, N, K, N2 = 128, 8512, 2048, 12288
+    M, K = 128, 2048
     g = torch.Generator(device="cpu").manual_seed(7)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
     W2 = (torch.randn(N2, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
     outs = []
     for n in (N, N2):
         Wpk = pack_weights(W2[:n].contiguous(), stream_ptr())
-        part = torch.empty(1, M, n, device=DEV)
-        call("zk_gemm_bf16", ptr(A), K, ptr(Wpk), M, n, K, 1, 0, ptr(part), None, None, stream_ptr())
-        outs.append(part[0, :, :N])
+        part = torch.empty(nsplit, M, n, device=DEV)
+        call("zk_gemm_bf16", ptr(A), K, ptr(Wpk), M, n, K, nsplit, 0, ptr(part), None, None, stream_ptr())
+        outs.append(part[:, :, :N])
     assert torch.equal(outs[0], outs[1])
 
 

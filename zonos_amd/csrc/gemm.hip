@@ -275,8 +275,11 @@ ZK_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory")
 // for NG times the weights (LDS reads and per-CU activation intake per weight byte / NG).
 // NB = activation fragment buffers (2: the next chunk's fragments are read while this one is
 // multiplied).
-template <int MODE, int NCH, int PF, int MT, int NCW = 4, int NG = 1, int NB = (NCW > 4 ? 1 : 2)>
-__global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
+// Loader waves: WS_NLD, fewer when that would put a ninth wave (a third per SIMD: 168 VGPRs) in the workgroup.
+template <int NCW>
+constexpr int ws_nld() { return NCW + WS_NLD > 8 ? 8 - NCW : WS_NLD; }
+template <int MODE, int NCH, int PF, int MT, int NCW = 4, int NG = 1, int NB = (NCW > 5 ? 1 : 2)>
+__global__ __launch_bounds__(64 * (NCW + ws_nld<NCW>()), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
                                                            bf16_t* __restrict__ Cout, const int32_t* skip,
@@ -296,12 +299,13 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ln = lane & 15, lg = lane >> 4;
 
+    constexpr int NLD = ws_nld<NCW>();
     if (w >= NCW) {
         // ---------------- loader wave(s): 2*MT x 1 KB LDS-DMA pieces per chunk (16*MT rows x 64 k),
-        // loader l moving pieces l, l + WS_NLD, ...
+        // loader l moving pieces l, l + NLD, ...
         // piece i covers tile rows 8i..8i+7; lane L lands at byte 16L of the piece:
         // row = 8i + (L>>3), slot = L&7  ->  source 16-B chunk = slot ^ (row&7)
-        constexpr int NP = (2 * MT + WS_NLD - 1) / WS_NLD;      // pieces per loader per chunk
+        constexpr int NP = (2 * MT + NLD - 1) / NLD;      // pieces per loader per chunk
         const int ld = __builtin_amdgcn_readfirstlane(w - NCW);   // wave-uniform: scalar piece loop
         const int rl = lane >> 3, sl = lane & 7;
         auto issue = [&](int ch) {
@@ -309,8 +313,8 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
             const int k0 = kbeg + ch * BK;
 #pragma unroll
             for (int j = 0; j < NP; ++j) {
-                const int i = j * WS_NLD + ld;
-                if (WS_NLD > 1 && i >= 2 * MT) break;          // (MT = 1, 2 loaders: 1 piece each)
+                const int i = j * NLD + ld;
+                if (NLD > 1 && i >= 2 * MT) break;          // (MT = 1, 2 loaders: 1 piece each)
                 const int row = 8 * i + rl;
                 const int m = min(row, M - 1);
                 const bf16_t* src = A + (size_t)m * lda + k0 + ((sl ^ (row & 7)) << 3);
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(64 * (NCW + WS_NLD), ZK_WS_OCC) void k_gemm_ws(cons
             // the loaders, idle from here on, stream their compute waves' first chunks into L2 (LDS-DMA
             // into the 1 KB sink past the ring), then keep the workgroup's barrier count: the epilogue's
             // two __syncthreads must not wait for these loads
-            warm_units(wW, wK, wgx, wgz, wch, blockIdx.x + gridDim.x * blockIdx.z, gridDim.x * gridDim.z, ld, WS_NLD,
+            warm_units(wW, wK, wgx, wgz, wch, blockIdx.x + gridDim.x * blockIdx.z, gridDim.x * gridDim.z, ld, NLD,
                        lane, smem + WS_NB * (MT * 16 * BK * 2));
             if (ZK_WS_EPI && (MODE == 1 || N % 4 == 0)) {
                 __builtin_amdgcn_s_barrier();
@@ -974,6 +978,10 @@ extern "C" int zk_pack_weights(const void* w, int N, int K, void* out, void* str
 #define ZK_WS_NARROW 3             // compute waves of the narrow workgroups for slab GEMMs with < 192 64-column tiles (0: off)
 #endif
 #define ZK_WS_NARROW_W (ZK_WS_NARROW > 0 ? ZK_WS_NARROW : 1)
+#ifndef ZK_WS_WIDE
+#define ZK_WS_WIDE 5               // compute waves of the wide workgroups for slab GEMMs with > 256 64-column tiles (0: off)
+#endif
+#define ZK_WS_WIDE_W (ZK_WS_WIDE > 0 ? ZK_WS_WIDE : 1)
 #ifndef ZK_WS_NARROW_BELOW
 #define ZK_WS_NARROW_BELOW 192     // ... when the 64-column grid has fewer workgroups than this
 #endif
@@ -1007,18 +1015,22 @@ bool zk_gemm_pf_applies(int M, int N, int K, int nsplit);
 int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int mode, float* C, void* Cb,
                const int32_t* skip, void* stream);
 
-// the narrow k_gemm_ws form (ZK_WS_NARROW compute waves per workgroup) for this slab GEMM?
-static bool ws_narrow(int M, int N, int nsplit, int mode, int ng) {
-    if (ZK_WS_NARROW <= 0 || ZK_WS_NCW != 4 || mode != 0 || M <= 64 || ng != 1) return false;
-    const long nnar = (long)(N + 16 * ZK_WS_NARROW - 1) / (16 * ZK_WS_NARROW) * nsplit;
-    return (long)((N + 63) / 64) * nsplit < ZK_WS_NARROW_BELOW && nnar <= 256;
+// k_gemm_ws compute waves per workgroup for this GEMM: 4 (64 columns), or for the slab GEMMs whose
+// 64-column grid fits the 256 CUs badly ZK_WS_NARROW (fewer than ZK_WS_NARROW_BELOW workgroups: more,
+// narrower ones) or ZK_WS_WIDE (more than 256: fewer, wider ones, so no CU runs two)
+static int ws_ncw(int M, int N, int nsplit, int mode, int ng) {
+    if (ZK_WS_NCW != 4 || mode != 0 || M <= 64 || ng != 1) return ZK_WS_NCW;
+    auto tiles = [&](int nw) { return (long)((N + 16 * nw - 1) / (16 * nw)) * nsplit; };
+    if (ZK_WS_NARROW > 0 && tiles(4) < ZK_WS_NARROW_BELOW && tiles(ZK_WS_NARROW) <= 256) return ZK_WS_NARROW;
+    if (ZK_WS_WIDE > 0 && tiles(4) > 256 && tiles(ZK_WS_WIDE) <= 256) return ZK_WS_WIDE;
+    return 4;
 }
 
 ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int mode, int chunks) {
     if (W == nullptr || M <= 16 || ZK_WS_NCW != 4 || !ws_regime(M, K, nsplit) || K % (nsplit * BK) != 0)
         return ZkWarm{nullptr, 0, 0, 0, 0};
     const int ng = ws_ng(N, mode);
-    const int nw = ws_narrow(M, N, nsplit, mode, ng) ? ZK_WS_NARROW : 4;
+    const int nw = ws_ncw(M, N, nsplit, mode, ng);
     return ZkWarm{W, K, (N + 16 * nw * ng - 1) / (16 * nw * ng), nsplit,
                   std::min(chunks, K / nsplit / BK) | (ng > 1 ? ng << 8 : 0) | (nw != 4 ? nw << 16 : 0)};
 }
@@ -1080,19 +1092,18 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
         // waves (16 columns each) while the grid still fits one workgroup per CU; the same
         // per-column K order (bit-identical results). (32 columns = 266 workgroups for 256 CUs:
         // c5 decode 4.34 -> 4.64 ms.)
-        const bool narrow = ws_narrow(M, N, nsplit, mode, ng);
-        const int ncw = narrow ? ZK_WS_NARROW : NCW;
+        const int ncw = M > 16 ? ws_ncw(M, N, nsplit, mode, ng) : NCW;
         dim3 g((N + 16 * ncw * ng - 1) / (16 * ncw * ng), 1, nsplit);
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
         const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2 + (warm.W ? 1024 : 0);     // + warm-up sink
 #define ZK_WS_LAUNCH5(MODE_, NCH_, MT_, NG_, NCW_)                                                                 \
     do {                                                                                                          \
-        constexpr int NB_ = NG_ > 1 ? ZK_WS_NGNB : (NCW_ > 4 ? 1 : 2);                                            \
+        constexpr int NB_ = NG_ > 1 ? ZK_WS_NGNB : (NCW_ > 5 ? 1 : 2);                                            \
         auto kern_ = &k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW_, NG_, NB_>;                       \
         if (lds > 65536)                                                                                          \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern_), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)lds);                                                                        \
-        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW_ + WS_NLD)), lds, (hipStream_t)stream,                        \
+        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW_ + ws_nld<NCW_>())), lds, (hipStream_t)stream,                \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
                            skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks);              \
         handled = true;                                                                                           \
@@ -1101,7 +1112,10 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
 #define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
     do {                                                                                                          \
         if ((MT_) == 8 && ng == 2) ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 2);                                            \
-        else if ((MODE_) == 0 && (MT_) == 8 && narrow) ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, ZK_WS_NARROW_W);          \
+        else if ((MODE_) == 0 && (MT_) == 8 && ncw == ZK_WS_NARROW_W && ncw != NCW)                                 \
+            ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, ZK_WS_NARROW_W);                                                    \
+        else if ((MODE_) == 0 && (MT_) == 8 && ncw == ZK_WS_WIDE_W && ncw != NCW)                                   \
+            ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, ZK_WS_WIDE_W);                                                      \
         else ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 1);                                                                  \
     } while (0)
 #define ZK_WS_LAUNCH(MODE_, NCH_)                                                                                  \
