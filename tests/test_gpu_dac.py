@@ -196,3 +196,26 @@ def test_c_dac_decode_long_equals_python_sequence(monkeypatch):
         monkeypatch.setattr(HipDacDecoder, "c_dac", flag)
         outs.append(dec.decode_padded(codes, lens).cpu())
     assert torch.equal(outs[0], outs[1])
+
+
+def test_dac_long_fused_units_equal_unfused_to_rounding(monkeypatch):
+    """The fused 96-channel residual units (zk_dac_resunit_cl) against the same decode with every unit
+    as two convs, at the multi-tile size: the 1x1 sums differ only in their fp32 grouping (16- vs
+    32-deep MFMA), so the waveforms agree far inside the north_star bar and both meet it."""
+    from zonos_amd.autoencoder import HipDacDecoder
+    from zonos_amd import _lib
+    dec, d, codes, wav, _ = _long()
+    assert _lib.load().zk_dac_resunit_supported(96) >= 1
+    # the fused unit's grid: 512-position tiles, one workgroup per CU -> >= 2 tiles each at this length
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert 2 * (-(-512 * codes.shape[2] // 512)) >= 2 * ncu
+    monkeypatch.setattr(HipDacDecoder, "c_dac", False)
+    outs = []
+    for fuse in (True, False):
+        monkeypatch.setattr(HipDacDecoder, "fuse_units", fuse)
+        outs.append(dec.decode_padded(codes).cpu())
+    diff = (outs[0] - outs[1]).pow(2).mean().sqrt().item()
+    assert diff <= 1e-5, diff
+    for o in outs:
+        for b in range(2):
+            assert (o[b] - wav[b]).pow(2).mean().sqrt().item() <= 1e-4
