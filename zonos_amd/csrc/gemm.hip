@@ -975,9 +975,8 @@ extern "C" int zk_pack_weights(const void* w, int N, int K, void* out, void* str
 #define ZK_WS_NCW 4                // k_gemm_ws compute waves (16-column tiles) per workgroup
 #endif
 #ifndef ZK_WS_NARROW
-#define ZK_WS_NARROW 3             // compute waves of the narrow workgroups for slab GEMMs with < 192 64-column tiles (0: off)
+#define ZK_WS_NARROW 2             // fewest compute waves of the narrow workgroups (2 or 3; 0: off)
 #endif
-#define ZK_WS_NARROW_W (ZK_WS_NARROW > 0 ? ZK_WS_NARROW : 1)
 #ifndef ZK_WS_WIDE
 #define ZK_WS_WIDE 5               // compute waves of the wide workgroups for slab GEMMs with > 256 64-column tiles (0: off)
 #endif
@@ -1021,7 +1020,9 @@ int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int 
 static int ws_ncw(int M, int N, int nsplit, int mode, int ng) {
     if (ZK_WS_NCW != 4 || mode != 0 || M <= 64 || ng != 1) return ZK_WS_NCW;
     auto tiles = [&](int nw) { return (long)((N + 16 * nw - 1) / (16 * nw)) * nsplit; };
-    if (ZK_WS_NARROW > 0 && tiles(4) < ZK_WS_NARROW_BELOW && tiles(ZK_WS_NARROW) <= 256) return ZK_WS_NARROW;
+    if (ZK_WS_NARROW > 0 && tiles(4) < ZK_WS_NARROW_BELOW)
+        for (int nw = ZK_WS_NARROW; nw <= 3; ++nw)          // the largest grid that still fits the CUs
+            if (tiles(nw) <= 256) return nw;
     if (ZK_WS_WIDE > 0 && tiles(4) > 256 && tiles(ZK_WS_WIDE) <= 256) return ZK_WS_WIDE;
     return 4;
 }
@@ -1088,10 +1089,10 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
         constexpr int NCW = ZK_WS_NCW;            // compute waves per workgroup
         const int ng = M > 16 && NCW == 4 ? ws_ng(N, mode) : 1;
         // a slab GEMM whose 64-column tiles x splits leave a quarter of the CUs idle (the c5 Mamba
-        // in_proj: N = 8512 unsplit, 133 tiles) runs narrower workgroups of ZK_WS_NARROW compute
-        // waves (16 columns each) while the grid still fits one workgroup per CU; the same
-        // per-column K order (bit-identical results). (32 columns = 266 workgroups for 256 CUs:
-        // c5 decode 4.34 -> 4.64 ms.)
+        // in_proj: N = 8512 unsplit, 133 tiles; the c3 out_proj, split 4: 128) runs narrower
+        // workgroups of 2 or 3 compute waves (16 columns each), the most that still fit one
+        // workgroup per CU (the Mamba in_proj at 2 waves would be 266 workgroups for 256 CUs:
+        // c5 decode 4.34 -> 4.64 ms); the same per-column K order (bit-identical results).
         const int ncw = M > 16 ? ws_ncw(M, N, nsplit, mode, ng) : NCW;
         dim3 g((N + 16 * ncw * ng - 1) / (16 * ncw * ng), 1, nsplit);
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
@@ -1112,8 +1113,10 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
 #define ZK_WS_LAUNCH3(MODE_, NCH_, MT_)                                                                            \
     do {                                                                                                          \
         if ((MT_) == 8 && ng == 2) ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 2);                                            \
-        else if ((MODE_) == 0 && (MT_) == 8 && ncw == ZK_WS_NARROW_W && ncw != NCW)                                 \
-            ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, ZK_WS_NARROW_W);                                                    \
+        else if ((MODE_) == 0 && (MT_) == 8 && ncw == 2 && NCW == 4)                                              \
+            ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, 2);                                                                 \
+        else if ((MODE_) == 0 && (MT_) == 8 && ncw == 3 && NCW == 4)                                              \
+            ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, 3);                                                                 \
         else if ((MODE_) == 0 && (MT_) == 8 && ncw == ZK_WS_WIDE_W && ncw != NCW)                                   \
             ZK_WS_LAUNCH5(MODE_, NCH_, MT_, 1, ZK_WS_WIDE_W);                                                      \
         else ZK_WS_LAUNCH4(MODE_, NCH_, MT_, 1);                                                                  \
