@@ -71,7 +71,7 @@ for step in "$@"; do
       python tools/pmc_summary.py "$OUT/attn_FETCH_SIZE" "$OUT/attn_WRITE_SIZE" --match "k_attn_decode<true" --R 128 \
           --ctx 1705 --alg 454033408 --json "$OUT/${rest}_attn_fused_pmc.json" > "$OUT/${rest}_attn_fused_pmc.txt"
       python tools/pmc_summary.py "$OUT/mamba_FETCH_SIZE" "$OUT/mamba_WRITE_SIZE" --match "k_mamba_step" --R 128 \
-          --ctx 0 --alg 288161792 --json "$OUT/${rest}_mamba_step_pmc.json" > "$OUT/${rest}_mamba_step_pmc.txt"
+          --ctx 0 --alg 283803648 --json "$OUT/${rest}_mamba_step_pmc.json" > "$OUT/${rest}_mamba_step_pmc.txt"
       find "$OUT" -name "*.csv" -path "*_SIZE*" -delete
       cat "$OUT/${rest}_attn_fused_pmc.json" "$OUT/${rest}_mamba_step_pmc.json" ;;
     prof)

@@ -225,8 +225,8 @@ def attn_small():
 
 def mamba():
     """Hybrid decode SSM update (zk_mamba_step) at c5 shapes: R=128 rows, 64 heads x 64 x 128 state,
-    in_proj split 2, rotating over 8 layers' states (1.1 GB: nothing stays in the MALL)."""
-    R, hp, ds, nh, gs = 128, 64, 128, 64, 2
+    in_proj unsplit (as the engine runs it at c5), rotating over 8 layers' states (1.1 GB: nothing stays in the MALL)."""
+    R, hp, ds, nh, gs = 128, 64, 128, 64, 1
     di = nh * hp
     conv_dim = di + 2 * ds
     ncol = 2 * di + 2 * ds + nh
