@@ -62,6 +62,37 @@ def gemm():
         del Ws
 
 
+def sweep():
+    """Fixed cost vs streamed bytes of the decode GEMM family: k_gemm_ws (M = 128, split 4) and the
+    B <= 8 GEMV (M = 2, split 1) at N = 2048 / 8192 over K = 512 .. 8192; fit t = t0 + bytes / rate."""
+    import numpy as np
+    for M, ns in ((128, 4), (2, 1)):
+        for N in (2048, 8192):
+            pts = []
+            for K in (512, 1024, 2048, 4096, 8192):
+                if M > 16 and K // ns // 64 > 32:
+                    continue
+                ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
+                Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+                A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+                part = torch.empty(ns * M * N, device=dev)
+                it = [0]
+
+                def f():
+                    W = Ws[it[0] % ncopy]
+                    it[0] += 1
+                    call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, ns, 0, ptr(part), None, None, S)
+                us = timeit(f)
+                pts.append((N * K * 2, us))
+                print(f"sweep M={M:3d} N={N:5d} K={K:5d} split={ns}: {us:7.2f} us  {N * K * 2 / 1e6:6.1f} MB  "
+                      f"{N * K * 2 / (us * 1e-6) / 1e9:6.0f} GB/s", flush=True)
+                del Ws
+            x = np.array([p[0] for p in pts], dtype=float)
+            y = np.array([p[1] for p in pts])
+            b, a = np.polyfit(x, y, 1)
+            print(f"fit   M={M:3d} N={N:5d}: fixed {a:5.2f} us + bytes at {1e-3 / b:5.2f} TB/s", flush=True)
+
+
 def warm():
     """Experiment: k_gemm_ws launches whose first weight chunks were just read into L2 by a small
     preceding kernel (zk_l2_warm_gemm) vs cold; time(pair) - time(warm kernel alone) vs time(cold)."""
@@ -344,6 +375,8 @@ if __name__ == "__main__":
         warm()
     if what in ("gemm", "all"):
         gemm()
+    if what == "sweep":
+        sweep()
     if what in ("mamba",):
         mamba()
     if what in ("attn_small",):
