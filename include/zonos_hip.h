@@ -212,10 +212,8 @@ typedef struct zk_gen_state {
  * [0,B) cond, [B,2B) uncond), bf16-rounded per head (model.py:111), CFG-combined
  * (model.py:112-115), biased (model.py:322-324,353,360-362) and sampled. prefill=1 is the
  * first sample (model.py:304: no bias, no penalty). draw 1 = EOS resample (model.py:386-393):
- * a no-op unless some row has a new EOS. draw 2 = both in one launch: tok0, and tok1 for every
- * (row, codebook) with codebook 0's EOS masked where that row's tok0 is a new EOS -- the values the
- * draw-1 launch writes when it runs (zk_eos_step takes tok1 only then). dbg_logits (nullable)
- * receives the fp32 CFG logits before bias [B][K][V]. */
+ * a no-op unless some row has a new EOS. dbg_logits (nullable) receives the fp32 CFG logits
+ * before bias [B][K][V]. */
 int zk_sample_heads(const float* part, int nsplit, const zk_gen_state* st, const zk_sampling_params* sp,
                     int prefill, int draw, float* dbg_logits, void* stream);
 /* EOS protocol + frame write + counters (model.py:376-424); prefill=1 only writes the

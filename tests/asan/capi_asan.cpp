@@ -120,11 +120,10 @@ static void transformer(int n_layer, int small, int merge) {
     CHECK(zk_decode_step(&d, nullptr) == 0, "zk_decode_step: %s", zk_last_error());
     // full step: both k_resid_ln and the fc1 GEMM of every layer warm the next GEMM's weights
     if (!small) CHECK(g_warm == 3 * n_layer, "L2 warm-up descriptors: %d", g_warm);
-    // embed + per layer (small: 5 with merge, 5 without; else 7) + heads + one sampler launch (both
-    // draws) + eos
+    // embed + per layer (small: 5 with merge, 5 without; else 7) + heads + 2 samples + eos
     const size_t per = small ? 5 : 7;
-    CHECK(g_calls.size() == 1 + per * n_layer + 3, "decode step: %zu calls", g_calls.size());
-    CHECK(count("zk_sample_heads") == 1 && count("zk_eos_step") == 1, "decode tail");
+    CHECK(g_calls.size() == 1 + per * n_layer + 4, "decode step: %zu calls", g_calls.size());
+    CHECK(count("zk_sample_heads") == 2 && count("zk_eos_step") == 1, "decode tail");
     if (!small) CHECK(count("zk_resid_ln") == (size_t)2 * n_layer, "resid_ln x2 per layer");
     if (small && merge) CHECK(count("zk_gemv_attn_out") == (size_t)n_layer, "merged out_proj per layer");
     // prefill
@@ -171,7 +170,7 @@ static void hybrid() {
     CHECK(zk_hybrid_decode_step(&d, nullptr) == 0, "zk_hybrid_decode_step: %s", zk_last_error());
     CHECK(count("zk_mamba_step") == 4 && count("zk_attn_decode_qkv") == 1 && count("zk_gated_rmsnorm") == 4,
           "hybrid layer sequence");
-    CHECK(g_calls.size() == 1 + 4 * 5 + 1 * 7 + 3, "hybrid step: %zu calls", g_calls.size());
+    CHECK(g_calls.size() == 1 + 4 * 5 + 1 * 7 + 4, "hybrid step: %zu calls", g_calls.size());
     g_calls.clear();
     CHECK(zk_hybrid_prefill(&d, P(0), 0, 4, P(0), nullptr) == 0, "zk_hybrid_prefill: %s", zk_last_error());
     CHECK(count("zk_mamba_prefill") == 4 && count("zk_attn_prefill") == 1, "hybrid prefill sequence");

@@ -448,47 +448,3 @@ def test_attention_out_proj_merge(R, ctx, nsplit):
     assert torch.equal(x1.view(torch.int16), x2.view(torch.int16)), (x1.float() - x2.float()).abs().max()
     # and the result is the attention + projection of an fp32 reference within bf16 tolerance
     assert not torch.equal(x1, x0)
-
-
-@pytest.mark.parametrize("sampling", ["cli", "greedy", "knobs"])
-@pytest.mark.parametrize("new_eos", [True, False])
-def test_sample_heads_both_draws_one_launch(sampling, new_eos):
-    """zk_sample_heads draw 2 (draws 0 and 1 in one launch, as the decode step runs it) writes the
-    tokens of a draw-0 launch followed by the draw-1 (EOS resample) launch: tok0 always, tok1
-    wherever the resample runs (some row with a new EOS: codebook 0 of that row with EOS masked)."""
-    import ctypes as C
-    from zonos_amd._lib import GenState, SamplingParams, call, ptr, stream_ptr
-    B, K, V, Ld, off, step = 6, 9, 1026, 40, 20, 5
-    g = torch.Generator(device="cpu").manual_seed(3 + int(new_eos))
-    logits = torch.randn(2 * B, K * V, generator=g) * 2.0
-    if new_eos:
-        logits[1, 1024] = 40.0          # row 1, codebook 0: EOS (new: eos_mode 0)
-    logits[4, 1024] = 40.0              # row 4 already in EOS mode: not new
-    part = logits.to(DEV)
-    delayed = torch.randint(0, 1024, (B, K, Ld), generator=g).to(DEV)
-    scal = torch.zeros(16, dtype=torch.int32, device=DEV)
-    scal[0], scal[1], scal[2] = off, off + 10, step
-    eos_mode = torch.tensor([0, 0, 0, 0, 1, 0], dtype=torch.int32, device=DEV)
-    z = lambda: torch.zeros(B, dtype=torch.int32, device=DEV)  # noqa: E731
-    act, rp = z(), torch.full((B,), 2.5, device=DEV)
-    sps = {"cli": (1.0, 0.0, 0.0, 0.65, 0.4, 0.0, 0, 8), "greedy": (0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0, 2),
-           "knobs": (0.8, 0.9, 0.05, 0.0, 0.0, 0.0, 50, 4)}[sampling]
-    sp = SamplingParams(*sps, 2.0, 0)
-    outs = []
-    for draws in ((0, 1), (2,)):
-        tok0 = torch.full((B * K,), -7, dtype=torch.int32, device=DEV)
-        tok1 = torch.full((B * K,), -7, dtype=torch.int32, device=DEV)
-        st = GenState(ptr(scal), ptr(eos_mode), ptr(z()), ptr(z()), ptr(z()), ptr(act), ptr(rp), ptr(tok0), ptr(tok1),
-                      ptr(delayed), B, K, Ld, V, 1234, 0)
-        for dr in draws:
-            call("zk_sample_heads", ptr(part), 1, C.byref(st), C.byref(sp), 0, dr, None, stream_ptr())
-        torch.cuda.synchronize()
-        outs.append((tok0.cpu(), tok1.cpu()))
-    (a0, a1), (b0, b1) = outs
-    assert torch.equal(a0, b0)
-    assert (a0.view(B, K)[1, 0].item() == 1024) == new_eos
-    if new_eos:
-        assert torch.equal(a1, b1)
-        assert a1.view(B, K)[1, 0].item() != 1024            # the resample masked EOS on the new-EOS row
-    else:
-        assert torch.all(a1 == -7)                           # no new EOS: the draw-1 launch wrote nothing

@@ -197,7 +197,8 @@ extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
     else
         ZK_STEP(zk_gemm_bf16(d->xn, D, d->heads, R, K * V, D, d->split_heads, 0, d->part, nullptr, skip, stream));
     const int nsp = d->small ? 1 : d->split_heads;
-    ZK_STEP(zk_sample_heads(d->part, nsp, &d->st, &d->sp, 0, 2, d->dbg, stream));   // draws 0 and 1
+    ZK_STEP(zk_sample_heads(d->part, nsp, &d->st, &d->sp, 0, 0, d->dbg, stream));
+    ZK_STEP(zk_sample_heads(d->part, nsp, &d->st, &d->sp, 0, 1, nullptr, stream));
     ZK_STEP(zk_eos_step(&d->st, 0, 0, stream));
     return 0;
 }
@@ -340,7 +341,8 @@ extern "C" int zk_hybrid_decode_step(const zk_hybrid_desc* d, void* stream) {
                            d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, d->xn, skip, stream));
     ZK_STEP(hybrid_layers(d, R, 1, false, nullptr, stream));
     ZK_STEP(zk_gemm_bf16(d->xn, D, d->heads, R, K * V, D, d->split_heads, 0, d->part, nullptr, skip, stream));
-    ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 0, 2, d->dbg, stream));   // draws 0 and 1
+    ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 0, 0, d->dbg, stream));
+    ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 0, 1, nullptr, stream));
     ZK_STEP(zk_eos_step(&d->st, 0, 0, stream));
     return 0;
 }

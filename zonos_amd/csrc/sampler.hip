@@ -208,9 +208,8 @@ struct RowCtx {
     uint64_t seed;
 };
 
-// Everything after the logits are in registers up to the race: rep-penalty, temperature, softmax and
-// the filters. Returns true for greedy sampling (T = 0: x still holds the penalised logits).
-ZK_DEV bool shape_row(float* x, const RowCtx& c, const zk_sampling_params& sp, Smem& s) {
+// Everything after the logits are in registers: rep-penalty, shaping, race / argmax.
+ZK_DEV int sample_row(float* x, const RowCtx& c, const zk_sampling_params& sp, Smem& s) {
     const int V = c.V;
     // ---- repetition penalty (sampling.py:142-169); rp == 1 is an exact identity
     if (c.gen != nullptr && sp.rp_window > 0) {
@@ -230,7 +229,7 @@ ZK_DEV bool shape_row(float* x, const RowCtx& c, const zk_sampling_params& sp, S
         }
         __syncthreads();
     }
-    if (!(sp.temperature > 0.f)) return true;                     // sampling.py:325-326: argmax
+    if (!(sp.temperature > 0.f)) return block_argmax(x, V, s);   // sampling.py:325-326
 
 #pragma unroll
     for (int i = 0; i < NPT; ++i) x[i] = __fdiv_rn(x[i], sp.temperature);
@@ -263,22 +262,13 @@ ZK_DEV bool shape_row(float* x, const RowCtx& c, const zk_sampling_params& sp, S
         for (int i = 0; i < NPT; ++i) if (x[i] < thr) x[i] = 0.f;
         renorm(x, V, s);
     }
-    return false;
-}
-
-// exponential race (sampling.py:26-28) with the noise of draw `draw`
-ZK_DEV int race_row(float* x, const RowCtx& c, int draw, Smem& s) {
+    // exponential race (sampling.py:26-28)
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
         const int v = threadIdx.x + NT * i;
-        if (v < c.V) x[i] = __fdiv_rn(x[i], exp_noise(c.seed, c.step, draw, c.row, c.k, v));
+        if (v < V) x[i] = __fdiv_rn(x[i], exp_noise(c.seed, c.step, c.draw, c.row, c.k, v));
     }
-    return block_argmax(x, c.V, s);
-}
-
-ZK_DEV int sample_row(float* x, const RowCtx& c, const zk_sampling_params& sp, Smem& s) {
-    if (shape_row(x, c, sp, s)) return block_argmax(x, c.V, s);
-    return race_row(x, c, c.draw, s);
+    return block_argmax(x, V, s);
 }
 
 __global__ __launch_bounds__(NT) void k_sample_logits(const float* logits, int B, int K, int V,
@@ -315,7 +305,6 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
     const int offset = scal[0], step = scal[2];
     const float rpb = st.rp[b];
     const int actb = st.act[b];
-    const int emb = st.eos_mode[b];
     int new_eos_b = 0;
     if (draw == 1) {   // EOS resample happens only if some row has a new EOS (model.py:380)
         int any = 0;   // one row per thread
@@ -363,7 +352,7 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
         x[i] = val;
     }
     if (done) return;                                       // generation finished
-    if (dbg != nullptr && draw != 1) {
+    if (dbg != nullptr && draw == 0) {
         float* d = dbg + ((size_t)b * K + k) * V;
 #pragma unroll
         for (int i = 0; i < NPT; ++i) { const int v = threadIdx.x + NT * i; if (v < V) d[v] = x[i]; }
@@ -383,39 +372,9 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
         }
     }
     RowCtx c{b, k, V, prefill ? nullptr : st.delayed + ((size_t)b * K + k) * st.Ld, offset,
-             prefill ? 1.f : rpb, prefill ? 0 : step, draw == 2 ? 0 : draw, st.row_base + b, st.seed};
-    if (draw != 2) {
-        const int t = sample_row(x, c, sp, s);
-        if (threadIdx.x == 0) (draw ? st.tok1 : st.tok0)[b * K + k] = t;
-        return;
-    }
-    // draw 2: both draws in one launch. Draw 1 (the EOS resample, model.py:380-390) sees the same
-    // logits except, for codebook 0 of a row whose draw-0 token is a new EOS, the EOS logit masked --
-    // and this workgroup holds that row's draw-0 token. So tok1 is sampled here for every (row,
-    // codebook) and k_eos_step takes it where any row has a new EOS, as it takes the separate
-    // draw-1 launch's tokens (identical values: same logits, same draw-1 noise).
-    float x0[NPT];
-#pragma unroll
-    for (int i = 0; i < NPT; ++i) x0[i] = x[i];
-    const bool greedy = shape_row(x, c, sp, s);
-    float pr[NPT];
-#pragma unroll
-    for (int i = 0; i < NPT; ++i) pr[i] = x[i];
-    const int t0 = greedy ? block_argmax(x, V, s) : race_row(x, c, 0, s);
-    int t1;
-    if (k == 0 && !prefill && t0 == EOS && !emb) {
-#pragma unroll
-        for (int i = 0; i < NPT; ++i)
-            if (threadIdx.x + NT * i == EOS) x0[i] = -INFINITY;                  // model.py:387
-        c.draw = 1;
-        t1 = sample_row(x0, c, sp, s);
-    } else {
-        t1 = greedy ? t0 : race_row(pr, c, 1, s);
-    }
-    if (threadIdx.x == 0) {
-        st.tok0[b * K + k] = t0;
-        st.tok1[b * K + k] = t1;
-    }
+             prefill ? 1.f : rpb, prefill ? 0 : step, draw, st.row_base + b, st.seed};
+    const int t = sample_row(x, c, sp, s);
+    if (threadIdx.x == 0) (draw ? st.tok1 : st.tok0)[b * K + k] = t;
 }
 
 // EOS protocol, frame write and step counters (model.py:376-424), one workgroup.
@@ -527,7 +486,6 @@ extern "C" int zk_sample_heads(const float* part, int nsplit, const zk_gen_state
                                void* stream) {
     ZK_REQUIRE(st && sp && part, "zk_sample_heads: null argument");
     ZK_REQUIRE(st->V > 0 && st->V <= NT * NPT, "zk_sample_heads: V=%d unsupported", st->V);
-    ZK_REQUIRE(draw >= 0 && draw <= 2 && !(prefill && draw != 0), "zk_sample_heads: draw=%d prefill=%d", draw, prefill);
     hipLaunchKernelGGL(k_sample_heads, dim3(st->B * st->K), dim3(NT), 0, (hipStream_t)stream, part, nsplit,
                        *st, *sp, prefill, draw, dbg_logits);
     ZK_CHECK_LAUNCH("zk_sample_heads");

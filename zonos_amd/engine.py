@@ -382,7 +382,8 @@ class HipDecoder(HipBackbone):
         else:
             self._layers(ws, R, R, 1, False, stream, skip)
             self._heads(ws, R, 1, stream, skip)
-        call("zk_sample_heads", ptr(logits), nsp, C_ref(st), C_ref(sp), 0, 2, ptr(ws["dbg"]), stream)   # draws 0, 1
+        call("zk_sample_heads", ptr(logits), nsp, C_ref(st), C_ref(sp), 0, 0, ptr(ws["dbg"]), stream)
+        call("zk_sample_heads", ptr(logits), nsp, C_ref(st), C_ref(sp), 0, 1, None, stream)
         call("zk_eos_step", C_ref(st), 0, 0, stream)
 
     def _small(self, R: int) -> bool:
