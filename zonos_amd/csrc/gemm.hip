@@ -332,7 +332,9 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW>()), ZK_WS_OCC) void k_gemm_
             // waves can read chunk c+1's fragments while they multiply chunk c)
             const int need = min(c + WS_LDSPF, nchunks - 1);
             const int younger = min(c - 1 + WS_DA, nchunks - 1) - need;   // chunks issued after `need`
-            if (younger >= 3) vm_wait<3 * NP>();
+            if (younger >= 5) vm_wait<5 * NP>();
+            else if (younger == 4) vm_wait<4 * NP>();
+            else if (younger == 3) vm_wait<3 * NP>();
             else if (younger == 2) vm_wait<2 * NP>();
             else if (younger == 1) vm_wait<NP>();
             else vm_wait<0>();
