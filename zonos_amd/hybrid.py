@@ -271,7 +271,9 @@ class HybridDecoder(HybridBackbone, HipDecoder):
         Mp = R * S_pre
         f32, bf, i32 = torch.float32, torch.bfloat16, torch.int32
         # Mamba in_proj (N = 8512, K = 2048) without split-K: 133 workgroups, no fp32 slab round trip
-        # for k_mamba_step (c5 decode step 4.67 vs 4.87 ms with 2 splits, 4.96 with 4; tools/c5_split_ab.sh)
+        # for k_mamba_step (c5 decode step 4.67 vs 4.87 ms with 2 splits, 4.96 with 4; tools/c5_split_ab.sh;
+        # round 4 with 80-column split-2 workgroups: the GEMM 15.3 -> 12.8 us alone, the step 4.34 -> 4.39 ms,
+        # profiles/r4s3_hyb_inp_split_ab.txt)
         # (attention out_proj 4-way and the heads unsplit, as the transformer engine: 4.645 vs 4.670 ms)
         splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R, target_blocks=128),
                       fc2=_split_for(D, max(Fd, 64), R), heads=1, inp=1, out=_split_for(D, di, R))
