@@ -95,6 +95,10 @@ int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, 
  * W is in the engine's fragment-packed layout (zk_pack_weights; rows padded to 64). */
 int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
                  float* Cpart, void* Cout, const int32_t* skip, void* stream);
+/* Host-only (no GPU): the number of 16-column tiles of W's packed image that the L2 warm-up of
+ * this decode GEMM (warm.h: issued by the kernel before it) reads; 0 when the GEMM is not warmed.
+ * Never more than ceil(N / 16), the tiles of the packed image that hold a column < N. */
+int zk_gemm_warm_tiles(int M, int N, int K, int nsplit, int mode, int chunks);
 /* Small-batch (M <= 16) GEMV without split-K, for the B <= 8 decode layer (five launches per
  * transformer block instead of seven; replaces the k_resid_ln launches of _torch.py:100-101):
  *   ln_w/ln_b non-NULL: A holds the residual rows x (bf16, K = D = 2048) and every workgroup

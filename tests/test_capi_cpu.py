@@ -67,6 +67,29 @@ def test_prefill_rejects_short_kv_cache_without_gpu(lib):
     assert b"KV cache" in lib.zk_last_error()
 
 
+def test_gemm_warm_up_stays_inside_packed_image(lib):
+    """The L2 warm-up a kernel issues for the next decode GEMM reads only tiles of that GEMM's packed
+    weight image (the 48-column workgroups of the c5 Mamba in_proj -- N = 8512, 178 x 3 =
+    534 tiles -- warmed 2 tiles past the 532-tile image). Every decode GEMM shape of c2-c5 at R = 128
+    and R = 24, each split the engine may pick."""
+    lib.zk_gemm_warm_tiles.restype = ctypes.c_int
+    shapes = [(3072, 2048), (2048, 2048), (16384, 2048), (2048, 8192), (9234, 2048), (8512, 2048),
+              (2048, 4096), (9280, 2048), (4400, 2048), (1000, 2048)]
+    seen_narrow = False
+    for M in (24, 72, 128):
+        for N, K in shapes:
+            for nsplit in (1, 2, 4, 8):
+                if K % (nsplit * 64) or K // nsplit // 64 > 32:
+                    continue
+                for mode in (0, 1):
+                    if mode == 1 and (nsplit != 1 or N % 16):
+                        continue
+                    t = lib.zk_gemm_warm_tiles(M, N, K, nsplit, mode, 2)
+                    assert 0 <= t <= (N + 15) // 16, (M, N, K, nsplit, mode, t)
+                    seen_narrow |= (N == 8512 and M == 128 and nsplit == 1 and t > 0)
+    assert seen_narrow
+
+
 def test_split_selection_batch_invariant():
     from zonos_amd.engine import _split_for
     for N, K in ((3072, 2048), (2048, 2048), (2048, 8192), (9234, 2048)):

@@ -151,3 +151,57 @@ def test_generate_sharded_single_process():
     got = generate_sharded(StubEngine(), cond, prefix, 8, 2.0, 4, {}, seed=3)
     ref = StubEngine().generate(cond, prefix, 8, 2.0, 4, {}, seed=3)
     assert all(torch.equal(a, b) for a, b in zip(got, ref))
+
+
+class RecordingStub(StubEngine):
+    """StubEngine that records the batch each generate() call ran (the GEMM regime is a function of it)."""
+
+    def __init__(self):
+        self.batches = []
+
+    def generate(self, cond, prefix, max_new, cfg_scale, B, sp, *, seed, row_base=0, **kw):
+        self.batches.append(B)
+        return super().generate(cond, prefix, max_new, cfg_scale, B, sp, seed=seed, row_base=row_base, **kw)
+
+
+def _ragged_worker(rank, world, port, q):
+    from zonos_amd.distributed import gemm_regime, generate_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B = 17
+    cond, prefix = _global_inputs(B)
+    eng = RecordingStub()
+    got = generate_sharded(eng, cond, prefix, 8, 2.0, B, {}, seed=5, coll_device="cpu")
+    ref = StubEngine().generate(cond, prefix, 8, 2.0, B, {}, seed=5)
+    ok = len(got) == B and all(torch.equal(a, b) for a, b in zip(got, ref))
+    q.put((rank, ok, eng.batches, [gemm_regime(b) for b in eng.batches]))
+    dist.destroy_process_group()
+
+
+def test_generate_sharded_ragged_keeps_one_regime():
+    """B = 17 over 2 ranks is a 9 + 8 split, i.e. M = 18 (k_gemm_ws) beside M = 16
+    (k_gemv): two reduction orders. The 8-utterance shard is padded to 9, so both ranks run the
+    k_gemm_ws regime at the same shape, and the gathered codes are still the one-batch codes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ragged_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] for r in res), res
+    assert [r[2] for r in res] == [[9], [9]], res
+    assert {g for r in res for g in r[3]} == {"ws"}, res
+
+
+def test_padded_shard_rule():
+    from zonos_amd.distributed import gemm_regime, padded_shard
+    for B in (1, 5, 17, 64, 511, 512):
+        for w in (1, 2, 3, 8):
+            runs = {padded_shard(B, w, r)[2] for r in range(w)} - {0}
+            assert len(runs) == 1
+            assert all(padded_shard(B, w, r)[2] - padded_shard(B, w, r)[1] <= 1 for r in range(w))
+    assert gemm_regime(8) == "gemv" and gemm_regime(9) == "ws" and gemm_regime(64) == "ws" and gemm_regime(65) == "gemm"

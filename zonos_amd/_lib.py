@@ -172,13 +172,15 @@ def load():
     lib.zk_dac_decode_workspace.argtypes = [C.POINTER(DacDesc), I, I]
     lib.zk_dac_resunit_supported.restype = C.c_int
     lib.zk_dac_resunit_supported.argtypes = [I]
+    lib.zk_gemm_warm_tiles.restype = C.c_int
+    lib.zk_gemm_warm_tiles.argtypes = [I, I, I, I, I, I]
     _lib = lib
     return lib
 
 
 def exported_symbols() -> list[str]:
     return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_abi_size",
-                          "zk_dac_decode_workspace", "zk_dac_resunit_supported"]
+                          "zk_dac_decode_workspace", "zk_dac_resunit_supported", "zk_gemm_warm_tiles"]
 
 
 def call(name: str, *args):

@@ -88,21 +88,26 @@ ZK_DEV void ws_tile(int L, int gx, int gz, int& bx, int& bz) {
 // `chunks` packs the GEMM's column groups per compute wave (k_gemm_ws NG) in bits 8+: wave w of
 // workgroup (bx, bz) streams the 16-row tiles (bx * 4 + w) * NG + g, g < NG.
 // chunks: bits 0-7 chunks per wave, 8-15 column groups per wave (NG, 0 = 1), 16-23 compute waves per
-// workgroup of the warmed GEMM (0 = 4)
-ZK_DEV int warm_nw(int chunks) { return (chunks >> 16) ? (chunks >> 16) : 4; }
+// workgroup of the warmed GEMM (0 = 4), 24-31 trailing 16-column tiles of its grid wholly past N
+// (the packed image holds ceil(N / 16) tiles, padded to 64 columns; a 48-column grid can overshoot
+// even that -- c5 Mamba in_proj: 178 x 3 = 534 tiles for a 532-tile image -- so those are skipped)
+ZK_DEV int warm_nw(int chunks) { return ((chunks >> 16) & 255) ? ((chunks >> 16) & 255) : 4; }
 ZK_DEV int warm_unit(const bf16_t* W, int K, int gx, int gz, int chunks, int L, int w, int lane, void* sink) {
     int bx, bz;
     ws_tile(L, gx, gz, bx, bz);
     const int ng = max(1, (chunks >> 8) & 255), nch = chunks & 255, nw = warm_nw(chunks);
+    const int ntiles = gx * nw * ng - ((chunks >> 24) & 255);      // 16-column tiles holding a column < N
     const int kbeg = bz * (K / gz);
     for (int g = 0; g < ng; ++g) {
-        const bf16_t* p = W + ((size_t)((bx * nw + w) * ng + g) * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
+        const int tile = (bx * nw + w) * ng + g;
+        if (tile >= ntiles) break;
+        const bf16_t* p = W + ((size_t)tile * (K >> 5) + (kbeg >> 5)) * 512 + lane * 8;
         for (int c = 0; c < nch; ++c) {
             __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024), sink, 16, 0, 0);
             __builtin_amdgcn_global_load_lds((const void*)(p + c * 1024 + 512), sink, 16, 0, 0);
         }
     }
-    return 2 * nch * ng;
+    return 0;
 }
 
 // All warm-up units of workgroup r of an nwg-workgroup launch (nwg % 8 == 0 keeps the GEMM

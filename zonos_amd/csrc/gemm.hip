@@ -275,11 +275,19 @@ ZK_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory")
 // for NG times the weights (LDS reads and per-CU activation intake per weight byte / NG).
 // NB = activation fragment buffers (2: the next chunk's fragments are read while this one is
 // multiplied).
-// Loader waves: WS_NLD, fewer when that would put a ninth wave (a third per SIMD: 168 VGPRs) in the workgroup.
-template <int NCW>
-constexpr int ws_nld() { return NCW + WS_NLD > 8 ? 8 - NCW : WS_NLD; }
+// Loader waves: WS_NLD, fewer when that would put a ninth wave (a third per SIMD: 168 VGPRs) in the
+// workgroup, and fewer again until every loader that issues pieces issues the same number of them
+// (2*MT pieces per chunk): each loader's counted vmcnt waits assume NP pieces per younger chunk, so
+// a loader with fewer would pass the publishing barrier with pieces of that chunk still in flight
+// (NCW = 5 at MT = 8: 3 loaders would split 16 pieces 6 / 5 / 5 -- 2 loaders split them 8 / 8).
+template <int NCW, int MT>
+constexpr int ws_nld() {
+    int n = NCW + WS_NLD > 8 ? 8 - NCW : WS_NLD;
+    while (n > 1 && n < 2 * MT && (2 * MT) % n != 0) --n;
+    return n;
+}
 template <int MODE, int NCH, int PF, int MT, int NCW = 4, int NG = 1, int NB = (NCW > 5 ? 1 : 2)>
-__global__ __launch_bounds__(64 * (NCW + ws_nld<NCW>()), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
+__global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
                                                            bf16_t* __restrict__ Cout, const int32_t* skip,
@@ -299,7 +307,9 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW>()), ZK_WS_OCC) void k_gemm_
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ln = lane & 15, lg = lane >> 4;
 
-    constexpr int NLD = ws_nld<NCW>();
+    constexpr int NLD = ws_nld<NCW, MT>();
+    static_assert(NLD >= 1 && (NLD >= 2 * MT || (2 * MT) % NLD == 0),
+                  "every loader wave must issue the same number of pieces per chunk (its vmcnt waits count NP)");
     if (w >= NCW) {
         // ---------------- loader wave(s): 2*MT x 1 KB LDS-DMA pieces per chunk (16*MT rows x 64 k),
         // loader l moving pieces l, l + NLD, ...
@@ -1034,8 +1044,30 @@ ZkWarm zk_gemm_warm_desc(const void* W, int M, int N, int K, int nsplit, int mod
         return ZkWarm{nullptr, 0, 0, 0, 0};
     const int ng = ws_ng(N, mode);
     const int nw = ws_ncw(M, N, nsplit, mode, ng);
-    return ZkWarm{W, K, (N + 16 * nw * ng - 1) / (16 * nw * ng), nsplit,
-                  std::min(chunks, K / nsplit / BK) | (ng > 1 ? ng << 8 : 0) | (nw != 4 ? nw << 16 : 0)};
+    const int gx = (N + 16 * nw * ng - 1) / (16 * nw * ng);
+    const int excess = gx * nw * ng - (N + 15) / 16;            // grid tiles wholly past N (< nw * ng)
+    return ZkWarm{W, K, gx, nsplit,
+                  std::min(chunks, K / nsplit / BK) | (ng > 1 ? ng << 8 : 0) | (nw != 4 ? nw << 16 : 0) |
+                      (excess << 24)};
+}
+
+// Host mirror of warm_unit's tile bound for the descriptor zk_gemm_warm_desc builds: the number of
+// 16-column tiles of the packed image the warm-up of this GEMM reads (0 when it is off). Tests check
+// it against ceil(N / 16), the tiles the packed image holds a column of (the 48-column
+// grid of the c5 Mamba in_proj once warmed 2 tiles past the image).
+extern "C" int zk_gemm_warm_tiles(int M, int N, int K, int nsplit, int mode, int chunks) {
+    static const char dummy = 0;
+    const ZkWarm d = zk_gemm_warm_desc(&dummy, M, N, K, nsplit, mode, chunks);
+    if (d.W == nullptr) return 0;
+    const int ng = std::max(1, (d.chunks >> 8) & 255), nw = ((d.chunks >> 16) & 255) ? ((d.chunks >> 16) & 255) : 4;
+    int hi = 0;
+    for (int bx = 0; bx < d.gx; ++bx)
+        for (int w = 0; w < nw; ++w)
+            for (int g = 0; g < ng; ++g) {
+                const int tile = (bx * nw + w) * ng + g;
+                if (tile < d.gx * nw * ng - ((d.chunks >> 24) & 255)) hi = std::max(hi, tile + 1);
+            }
+    return hi;
 }
 
 extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
@@ -1106,7 +1138,7 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
         if (lds > 65536)                                                                                          \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern_), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)lds);                                                                        \
-        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW_ + ws_nld<NCW_>())), lds, (hipStream_t)stream,                \
+        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW_ + ws_nld<NCW_, MT_>())), lds, (hipStream_t)stream,                \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
                            skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks);              \
         handled = true;                                                                                           \

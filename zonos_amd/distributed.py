@@ -60,6 +60,35 @@ def gather_codes(codes: list, device=None, group=None) -> list:
     return out
 
 
+def gemm_regime(batch: int) -> str:
+    """The decode GEMM regime of a batch of utterances (2 CFG rows each), DESIGN.md §4: split counts
+    depend on (N, K) only, but the reduction ORDER differs between regimes -- ``"gemv"`` (M <= 16,
+    k_gemv_* K quarters), ``"ws"`` (16 < M <= 128, k_gemm_ws sequential K), ``"gemm"`` (M > 128)."""
+    m = 2 * batch
+    return "gemv" if m <= 16 else ("ws" if m <= 128 else "gemm")
+
+
+def padded_shard(global_batch: int, world: int, rank: int) -> tuple[int, int, int]:
+    """(row_base, local_batch, run_batch): the rank's contiguous block and the batch it actually
+    runs. Blocks differ by at most one utterance, so a ragged split (B = 17 over 2 ranks: 9 + 8)
+    would run M = 18 (k_gemm_ws) on one rank and M = 16 (k_gemv) on the other -- two reduction orders.
+    Every non-empty block is padded to the largest block size instead, so all ranks run the same
+    kernels on the same shapes; an empty block stays empty."""
+    row_base, local = shard(global_batch, world, rank)
+    most = -(-global_batch // world)
+    return row_base, local, (most if local > 0 else 0)
+
+
+def _pad_rows(x: torch.Tensor, local: int, run: int, cfg_pairs: bool) -> torch.Tensor:
+    """Append run - local copies of the last utterance (of each CFG half when ``cfg_pairs``)."""
+    if run == local:
+        return x
+    if not cfg_pairs:
+        return torch.cat([x, x[local - 1:local].expand(run - local, *x.shape[1:])])
+    c, u = x[:local], x[local:]
+    return torch.cat([c, c[-1:].expand(run - local, *x.shape[1:]), u, u[-1:].expand(run - local, *x.shape[1:])])
+
+
 def _split_rows(cond: torch.Tensor, global_batch: int, row_base: int, local: int) -> torch.Tensor:
     """This rank's CFG rows of a global [2B, Lc, D] conditioning: cond rows [rb, rb+n) and their
     uncond partners [B+rb, B+rb+n) (model.py:113, 213-218 keep each pair B rows apart)."""
@@ -70,7 +99,7 @@ def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_code
                      max_new_tokens: int = 86 * 30, cfg_scale: float = 2.0, batch_size: int = 1,
                      sampling_params: dict | None = None, *, seed: int | None = None, group=None,
                      gather: bool = True, local_input: bool = False, coll_device=None, return_local: bool = False,
-                     **generate_kw):
+                     uniform_shards: bool = True, **generate_kw):
     """Zonos.generate (model.py:224-457) of a GLOBAL batch of ``batch_size`` utterances sharded over
     the ranks of ``group`` (one process per GPU) -- the library form of zonos_batch_cli.py:113-162's
     batching with the batch split across the node's GPUs.
@@ -84,6 +113,9 @@ def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_code
     * ``seed`` None draws one seed on rank 0 from torch's generator and broadcasts it.
     * ``coll_device`` None runs the collectives on the group's device (`collective_device`: the
       current GPU under nccl, the CPU under gloo).
+    * ``uniform_shards`` (default) pads a block that is one utterance short of the largest block with
+      a copy of its last utterance (its codes are dropped), so every rank runs the same GEMM regime
+      and shapes (`padded_shard`); an exactly divisible batch (the benchmark's 64 per GPU) pads nothing.
     * No collective touches the decode; with ``gather`` one all_gather of the int32 codes returns
       the global list (utterance order) on every rank, else the rank's own list;
       ``return_local`` returns (the rank's own list on its device, the gathered list).
@@ -92,7 +124,9 @@ def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_code
     ``model.generate`` on the whole batch."""
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if world > 1 else 0
-    row_base, local = shard(batch_size, world, rank)
+    row_base, local, run = padded_shard(batch_size, world, rank)
+    if not uniform_shards or world == 1:
+        run = local
     if world > 1 and coll_device is None:
         coll_device = collective_device(group)
     if world > 1 and seed is None:
@@ -112,8 +146,12 @@ def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_code
     if local == 0:
         codes = []
     else:
-        codes = model.generate(cond, prefix, max_new_tokens, cfg_scale, local, sampling_params, seed=seed,
-                               row_base=row_base, **generate_kw)
+        if run != local:
+            cond = _pad_rows(cond, local, run, cfg_pairs=True)
+            if prefix is not None:
+                prefix = _pad_rows(prefix, local, run, cfg_pairs=False)
+        codes = model.generate(cond, prefix, max_new_tokens, cfg_scale, run, sampling_params, seed=seed,
+                               row_base=row_base, **generate_kw)[:local]
     if world == 1 or not gather:
         allc = codes
     else:

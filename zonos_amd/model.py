@@ -66,11 +66,17 @@ class Zonos:
     @classmethod
     def from_local(cls, config_path: str, model_path: str, device=DEFAULT_DEVICE, backbone: str | None = None,
                    autoencoder: DACAutoencoder | None = None) -> "Zonos":
-        """model.py:65-88. ``backbone`` selects a class of the registry (zonos_amd.backbone.BACKBONES,
-        the reference's keys included) exactly as the reference does: an unknown name raises KeyError,
-        and a class whose ``supported_architectures`` lacks the checkpoint's architecture raises
-        ValueError (the reference's torch backbone asserts on a hybrid config, _torch.py:56). The
-        selected plugin runs the same kernels as the engine, so generate() is unchanged by it."""
+        """model.py:65-88. ``backbone`` names a class of the registry (zonos_amd.backbone.BACKBONES,
+        the reference's keys included) and is **validated only**: an unknown name raises KeyError, and a
+        class whose ``supported_architectures`` lacks the checkpoint's architecture raises ValueError
+        (the reference's torch backbone asserts on a hybrid config, _torch.py:56). The model is then
+        built on the engine of the checkpoint's architecture whatever the name -- ``HipDecoder`` for a
+        transformer, ``HybridDecoder`` for a hybrid -- because every registered plugin runs exactly those
+        kernels for that architecture (``HipHybridBackbone`` on a transformer config runs the transformer
+        blocks, zonos_amd/backbone.py), so generate() does not depend on the selection. The name is kept
+        in ``model.backbone_name``. (One deviation: the reference's mamba_ssm backbone, selected
+        explicitly for a transformer checkpoint, would build mamba_ssm MHA blocks; here the transformer
+        blocks run, as with the reference's default choice for a transformer config, model.py:70-75.)"""
         from safetensors import safe_open
 
         from .backbone import BACKBONES
