@@ -155,6 +155,66 @@ def attn_roofline(eng, ctx):
                  ctx=ctx, attn_splits=ws["attn_splits"], layers="rotating over all attention layers' caches")
 
 
+def gemm_roofline(eng):
+    """The decode step's weight GEMMs (k_gemm_ws, 16 < R <= 128) and split-K slab reduces (k_resid_ln),
+    each launched as the step launches it (same shapes, splits and kernels) over the 26 layers'
+    weights in turn, timed with HIP events; algorithmic bytes = weights + activation + output once
+    (tools/gemm_pmc.py alg_bytes / reduce_bytes); traffic = PMC HBM bytes per launch of the same
+    kernel at the same shape (profiles/*gemm_pmc*.json: FETCH_SIZE x2 + WRITE_SIZE). Isolated
+    launches: inside the step the L2 warm-up by the kernel before each GEMM shortens it further."""
+    from zonos_amd._lib import call, ptr
+    ws, c = eng._ws, eng.cfg
+    R, D, H, Hk, hd, Fd = ws["R"], c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
+    sp = ws["splits"]
+    Nq = (H + 2 * Hk) * hd
+    part, h, xn, x, y = ws["part"], ws["h"], ws["xn"], ws["x"], ws["y"]
+    gemms = [("in_proj", "wqkv", xn, Nq, D, sp["qkv"], 0), ("out_proj", "wo", y, D, H * hd, sp["o"], 0),
+             ("fc1", "fc1", xn, 2 * Fd, D, 1, 1), ("fc2", "fc2", h, D, Fd, sp["fc2"], 0)]
+    out = {}
+    for name, key, A, N, K, ns, mode in gemms:
+        def launch(L, A=A, N=N, K=K, ns=ns, mode=mode, key=key):
+            return lambda st: call("zk_gemm_bf16", ptr(A), K, ptr(L[key]), R, N, K, ns, mode, ptr(part), ptr(h), None,
+                                   st)
+        per = _time_launches([launch(L) for L in eng.layers], reps=2)
+        b = N * K * 2 + R * K * 2 + (R * N * 4 * ns if mode == 0 else R * (N // 2) * 2)
+        out[name] = dict(M=R, N=N, K=K, nsplit=ns, bytes=int(b), us=round(per * 1e6, 2),
+                         frac=round(b / per / 1e9 / HBM_PEAK_GBS, 4),
+                         traffic_ratio=_pmc_field("k_gemm_ws", "traffic_ratio", name=name, M=R))
+    Nh = 9 * 1026
+    per = _time_launches([lambda st: call("zk_gemm_bf16", ptr(xn), D, ptr(eng.heads), R, Nh, D, sp["heads"], 0,
+                                          ptr(part), None, None, st)], reps=8)
+    b = Nh * D * 2 + R * D * 2 + R * Nh * 4 * sp["heads"]
+    out["heads"] = dict(M=R, N=Nh, K=D, nsplit=sp["heads"], bytes=int(b), us=round(per * 1e6, 2),
+                        frac=round(b / per / 1e9 / HBM_PEAK_GBS, 4),
+                        traffic_ratio=_pmc_field("k_gemm_ws", "traffic_ratio", name="heads", M=R))
+    for ns in sorted({sp["o"], sp["fc2"]}):
+        def launch(L, ns=ns):
+            return lambda st: call("zk_resid_ln", ptr(part), ns, ptr(x), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, R, D,
+                                   ptr(x), ptr(xn), 0, None, st)
+        per = _time_launches([launch(L) for L in eng.layers], reps=2)
+        b = ns * R * D * 4 + R * D * 2 + 2 * D * 2 + 2 * R * D * 2
+        out[f"resid_ln{ns}"] = dict(M=R, nsplit=ns, bytes=int(b), us=round(per * 1e6, 2),
+                                    frac=round(b / per / 1e9 / HBM_PEAK_GBS, 4),
+                                    traffic_ratio=_pmc_field("k_resid_ln", "traffic_ratio", name=f"resid_ln{ns}", M=R))
+    per_step = 26 * sum(v["us"] for k, v in out.items() if k != "heads") + out["heads"]["us"]
+    return dict(unit="us / launch (isolated)", peak_gbs=HBM_PEAK_GBS, per_step_us=round(per_step, 1), **out)
+
+
+def _pmc_field(kernel_prefix: str, field: str, **shape):
+    """A field of the committed PMC summary entry matching the kernel prefix and shape (or None)."""
+    import glob
+    found = None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+        for e in (d if isinstance(d, list) else [d]):
+            if str(e.get("kernel", "")).startswith(kernel_prefix) and all(e.get(k) == v for k, v in shape.items()):
+                found = e.get(field)
+    return found
+
+
 def gemv_roofline(eng):
     """B <= 8 (c2): the largest launch of the small-batch step -- fc1 with the norm2 LayerNorm
     prologue and the SwiGLU epilogue (zk_gemv_fused -> k_gemv_f), launched as _layers_small
@@ -369,7 +429,10 @@ class GpuWorkload:
                          frac=round(sb / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                          note="algorithmic bytes per decode step at the mean context / (generate wall time / decode "
                               "steps, prefill included)")
-        return dict(roofline=roof, step_roofline=step_roof,
+        extra = {}
+        if args.model != "hybrid" and not eng._small(R) and R <= 128:
+            extra["gemm_roofline"] = gemm_roofline(eng)
+        return dict(roofline=roof, step_roofline=step_roof, **extra,
                     breakdown={"generate_s_per_step": round(gen_step_s, 3),
                                "dac_s_per_step": round(self.stats["dac_s"] / args.steps, 3),
                                "dac_precision": self.dac.precision if self.dac is not None else None,

@@ -80,8 +80,12 @@ int zk_layernorm(const void* x, const void* w, const void* b, float eps, int row
                  void* y, void* stream);
 
 /* x_out = bf16(x_in + bf16(sum_s part[s])) ; xn = LayerNorm(x_out) (_torch.py:100-101).
- * ln_on_sum = 1: xn = LayerNorm(x_in + bf16(sum)) of the fp32 sum before rounding (mamba_ssm
- * layer_norm_fn with prenorm, the hybrid backbone's fused add + norm).
+ * ln_on_sum is a flags word. Bit 0: xn = LayerNorm(x_in + bf16(sum)) of the fp32 sum before rounding
+ * (mamba_ssm layer_norm_fn with prenorm, the hybrid backbone's fused add + norm). With bit 0 set, the
+ * hybrid config variants (mamba_ssm Block, _mamba_ssm.py:18-31,49-57): bit 1 RMS norm
+ * (is_rms_norm: y = x * rsqrt(mean(x^2) + eps) * w (+ b); b may be NULL), bit 2 x_in is fp32, bit 3
+ * x_out is fp32 (residual_in_fp32), and nsplit = 0 adds no projection (part unused: the first
+ * block's norm of the embedding, layer_norm_fn with residual = None).
  * part: fp32 [nsplit][rows][D] split-K slabs of the preceding projection. */
 int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, const void* b,
                 float eps, int rows, int D, void* x_out, void* xn_out, int ln_on_sum,
@@ -290,19 +294,22 @@ int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P, void* q, 
  *                  zk_gated_rmsnorm -> out_proj GEMM -> zk_resid_ln(ln_on_sum = 1, next norm)
  *   attention    : Wqkv GEMM -> zk_attn_decode_qkv (GPT-NeoX RoPE) -> out_proj -> zk_resid_ln(norm2)
  *                  -> fc1 (SwiGLU) -> fc2 -> zk_resid_ln(next norm)
+ * (a Mamba2 block with d_mlp > 0 continues like the attention block from zk_resid_ln(norm2); with
+ * norm_flags != 0 the first block's norm is its own zk_resid_ln(nsplit = 0) after the embedding)
  * then norm_f, the 9 heads, the sampler and the EOS protocol exactly as zk_decode_step. Conv and
  * SSM states are double-buffered by step parity ({a, b}, zk_mamba_step). Replaces the
  * `_decode_one_token` / `_prefill` bodies of model.py:118-202 for the mamba_ssm backbone (the one
  * the reference CUDA-graph-captures, model.py:220-222). */
 typedef struct zk_hybrid_layer {
     int32_t type;           /* 0 attention block, 1 Mamba2 block */
-    int32_t pad_;
-    const void* ln1_w;      /* norm.weight / bias (bf16 [D]) */
+    int32_t d_mlp;          /* Mamba2 block: GatedMLP width (d_intermediate; 0 = no norm2 / MLP, the
+                               Zonos-v0.1-hybrid case); attention block: 0 = d_ff of the descriptor */
+    const void* ln1_w;      /* norm.weight / bias (bf16 [D]; ln1_b NULL under rms_norm) */
     const void* ln1_b;
-    /* attention block */
+    /* attention block (norm2 / mlp also of a Mamba2 block with d_mlp > 0) */
     const void* wqkv;       /* mixer.in_proj, packed */
     const void* wo;         /* mixer.out_proj, packed */
-    const void* ln2_w;      /* norm2 */
+    const void* ln2_w;      /* norm2 (ln2_b NULL under rms_norm: bias-free RMSNorm) */
     const void* ln2_b;
     const void* fc1;        /* mlp.fc1 (zk_permute_fc1 order), packed */
     const void* fc2;        /* mlp.fc2, packed */
@@ -324,7 +331,10 @@ typedef struct zk_hybrid_layer {
 typedef struct zk_hybrid_desc {
     int32_t B, n_layer, d_model, n_heads, n_kv, head_dim, d_ff, smax;
     int32_t d_inner, nheads_ssm, headdim_ssm, d_state;
-    int32_t split_qkv, split_o, split_fc2, split_heads, split_inp, split_out, attn_splits, pad_;
+    int32_t split_qkv, split_o, split_fc2, split_heads, split_inp, split_out, attn_splits;
+    int32_t norm_flags;            /* BackboneConfig variants: bit 1 rms_norm (block norms are bias-free
+                                      RMSNorms, norm_f an RMS norm with its bias), bit 2 residual_in_fp32
+                                      (residual stream in xf, fp32); 0 = Zonos-v0.1-hybrid */
     float eps;                     /* LayerNorm eps (norm_epsilon) */
     float gate_eps;                /* RMSNormGated eps (1e-5 in mamba_ssm Mamba2) */
     const zk_hybrid_layer* layers; /* [n_layer] */
@@ -345,6 +355,7 @@ typedef struct zk_hybrid_desc {
     float* dbg;                    /* nullable: fp32 CFG logits of draw 0 */
     zk_gen_state st;
     zk_sampling_params sp;
+    void* xf;                      /* residual rows fp32 [rows][D] (norm_flags bit 2; else unused) */
 } zk_hybrid_desc;
 
 int zk_hybrid_decode_step(const zk_hybrid_desc* d, void* stream);

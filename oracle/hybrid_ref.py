@@ -22,6 +22,14 @@ config.json is not here. This module restates their published
     out_proj.
   Final: LayerNorm(hidden + residual).
 
+  Config variants (BackboneConfig fields that create_block and the final layer_norm_fn honour,
+  _mamba_ssm.py:18-31,49-57; restated from mamba_ssm 2.2.4 Block / GatedMLP / layer_norm_fn):
+    rms_norm: block norms are RMSNorm (weight only); layer_norm_fn(is_rms_norm=True) computes
+      rstd = 1 / sqrt(mean(x^2) + eps), y = x * rstd * w (+ b: norm_f keeps its LayerNorm bias).
+    residual_in_fp32: the residual stream is fp32 (the first block's residual_out = fp32(hidden);
+      later blocks keep the fp32 residual they are given); hidden + residual is added in fp32.
+    d_intermediate != 0: Mamba2 blocks get norm2 + GatedMLP(d_intermediate rounded up to 128) too.
+
 Parity with the real hybrid is UNPINNED (no mamba_ssm, no checkpoint, no config here); the
 prefill scan is run as the exact recurrence (the reference's SSD chunked scan computes the same
 recurrence with a different summation order).
@@ -54,6 +62,12 @@ class HybridCfg:
     eps: float = 1e-5
     n_cb: int = 9
     vocab: int = 1026
+    d_mlp: int = 0                                  # d_intermediate: GatedMLP width of the Mamba2 blocks
+    rms_norm: bool = False
+    residual_in_fp32: bool = False
+
+    def mlp_width(self, i: int) -> int:
+        return self.d_ff if self.is_attn(i) else self.d_mlp
 
     @property
     def head_dim(self):
@@ -84,18 +98,18 @@ class HybridCfg:
         a, s = b.get("attn_cfg", {}), dict(b.get("ssm_cfg", {}))
         assert s.pop("layer", "Mamba2") == "Mamba2", "only Mamba2 SSM layers"
         assert not a.get("qkv_proj_bias", False) and not a.get("out_proj_bias", False), "biased MHA not supported"
-        assert b.get("d_intermediate", 0) == 0, "MLP on Mamba layers not supported"
-        assert not b.get("rms_norm", False) and not b.get("residual_in_fp32", False)
-        return cls(d_model=b["d_model"], n_layer=b["n_layer"], attn_layer_idx=tuple(b.get("attn_layer_idx", [])),
+        r128 = lambda n: (n + 127) // 128 * 128 if n else 0     # GatedMLP multiple_of = 128
+        return cls(d_mlp=r128(b.get("d_intermediate", 0)), rms_norm=bool(b.get("rms_norm", False)),
+                   residual_in_fp32=bool(b.get("residual_in_fp32", False)),d_model=b["d_model"], n_layer=b["n_layer"], attn_layer_idx=tuple(b.get("attn_layer_idx", [])),
                    n_heads=a.get("num_heads", 16), n_kv=a.get("num_heads_kv", a.get("num_heads", 16)),
-                   d_ff=b.get("attn_mlp_d_intermediate", 0), d_state=s.get("d_state", 128),
+                   d_ff=r128(b.get("attn_mlp_d_intermediate", 0)), d_state=s.get("d_state", 128),
                    d_conv=s.get("d_conv", 4), expand=s.get("expand", 2), headdim=s.get("headdim", 64),
                    ngroups=s.get("ngroups", 1), rotary_base=a.get("rotary_emb_base", 10000.0),
                    eps=b.get("norm_epsilon", 1e-5))
 
     def to_zonos_config(self) -> dict:
         return {
-            "backbone": {"d_model": self.d_model, "d_intermediate": 0, "attn_mlp_d_intermediate": self.d_ff,
+            "backbone": {"d_model": self.d_model, "d_intermediate": self.d_mlp, "attn_mlp_d_intermediate": self.d_ff,
                          "n_layer": self.n_layer, "ssm_cfg": {"layer": "Mamba2", "d_state": self.d_state, "d_conv": self.d_conv,
                                                                  "expand": self.expand, "headdim": self.headdim,
                                                                  "ngroups": self.ngroups},
@@ -103,7 +117,8 @@ class HybridCfg:
                          "attn_cfg": {"causal": True, "num_heads": self.n_heads, "num_heads_kv": self.n_kv,
                                       "rotary_emb_dim": self.head_dim, "qkv_proj_bias": False,
                                       "out_proj_bias": False},
-                         "rms_norm": False, "residual_in_fp32": False, "norm_epsilon": self.eps},
+                         "rms_norm": self.rms_norm, "residual_in_fp32": self.residual_in_fp32,
+                         "norm_epsilon": self.eps},
             "prefix_conditioner": {"conditioners": [], "projection": "none"},
             "eos_token_id": 1024, "masked_token_id": 1025, "pad_vocab_to_multiple_of": 8,
         }
@@ -121,15 +136,12 @@ def weight_shapes(c: HybridCfg) -> dict:
     for i in range(c.n_layer):
         p = f"backbone.layers.{i}."
         s[p + "norm.weight"] = (D,)
-        s[p + "norm.bias"] = (D,)
+        if not c.rms_norm:
+            s[p + "norm.bias"] = (D,)
         if c.is_attn(i):
             hd = c.head_dim
             s[p + "mixer.in_proj.weight"] = ((c.n_heads + 2 * c.n_kv) * hd, D)
             s[p + "mixer.out_proj.weight"] = (D, c.n_heads * hd)
-            s[p + "norm2.weight"] = (D,)
-            s[p + "norm2.bias"] = (D,)
-            s[p + "mlp.fc1.weight"] = (2 * c.d_ff, D)
-            s[p + "mlp.fc2.weight"] = (D, c.d_ff)
         else:
             s[p + "mixer.in_proj.weight"] = (c.d_in_proj, D)
             s[p + "mixer.conv1d.weight"] = (c.conv_dim, 1, c.d_conv)
@@ -139,6 +151,14 @@ def weight_shapes(c: HybridCfg) -> dict:
             s[p + "mixer.D"] = (c.nheads_ssm,)
             s[p + "mixer.norm.weight"] = (c.d_inner,)
             s[p + "mixer.out_proj.weight"] = (D, c.d_inner)
+        # (after the mixer: make_weights draws in this order, so the default geometry's seeded weights
+        # -- and the fixtures' checksums -- are those of the round-4 layout)
+        if c.mlp_width(i):
+            s[p + "norm2.weight"] = (D,)
+            if not c.rms_norm:
+                s[p + "norm2.bias"] = (D,)
+            s[p + "mlp.fc1.weight"] = (2 * c.mlp_width(i), D)
+            s[p + "mlp.fc2.weight"] = (D, c.mlp_width(i))
     s["backbone.norm_f.weight"] = (D,)
     s["backbone.norm_f.bias"] = (D,)
     return s
@@ -214,11 +234,21 @@ class HybridCache:
         self.lengths = torch.zeros(rows, dtype=torch.int32)
 
 
-def add_norm(x, residual, w, b, eps):
-    """layer_norm_fn(..., prenorm=True, residual_in_fp32=False)."""
+def norm(s, w, b, eps, rms: bool = False):
+    """layer_norm_fn's normalisation of the fp32 sum s -> bf16: LayerNorm, or is_rms_norm
+    (y = s * rsqrt(mean(s^2) + eps) * w, + b when there is a bias)."""
+    if not rms:
+        return F.layer_norm(s, (s.shape[-1],), w.float(), b.float(), eps).to(bf)
+    y = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return (y if b is None else y + b.float()).to(bf)
+
+
+def add_norm(x, residual, w, b, eps, rms: bool = False, resid_f32: bool = False):
+    """layer_norm_fn(..., prenorm=True, residual_in_fp32, is_rms_norm): hidden + residual in fp32,
+    the residual returned in fp32 (residual_in_fp32, or a fp32 residual given) or bf16."""
     s = x.float() if residual is None else x.float() + residual.float()
-    y = F.layer_norm(s, (s.shape[-1],), w.float(), b.float(), eps).to(bf)
-    return y, s.to(bf)
+    keep32 = resid_f32 or (residual is not None and residual.dtype == torch.float32)
+    return norm(s, w, b, eps, rms), (s if keep32 else s.to(bf))
 
 
 def mha(W, c: HybridCfg, i, x, cache: HybridCache, rot):
@@ -286,18 +316,18 @@ def mamba2(W, c: HybridCfg, i, u, cache: HybridCache):
 
 def backbone(W, c: HybridCfg, h: torch.Tensor, cache: HybridCache, rot: torch.Tensor) -> torch.Tensor:
     """MambaSSMZonosBackbone.forward (_mamba_ssm.py:47-57)."""
-    D = c.d_model
     hidden, residual = h, None
+    kw = dict(rms=c.rms_norm, resid_f32=c.residual_in_fp32)
     for i in range(c.n_layer):
         p = f"backbone.layers.{i}."
-        xn, residual = add_norm(hidden, residual, W[p + "norm.weight"], W[p + "norm.bias"], c.eps)
+        xn, residual = add_norm(hidden, residual, W[p + "norm.weight"], W.get(p + "norm.bias"), c.eps, **kw)
         if c.is_attn(i):
             hidden = mha(W, c, i, xn, cache, rot)
-            xn, residual = add_norm(hidden, residual, W[p + "norm2.weight"], W[p + "norm2.bias"], c.eps)
-            y, gate = F.linear(xn, W[p + "mlp.fc1.weight"]).chunk(2, dim=-1)
-            hidden = F.linear(y * F.silu(gate), W[p + "mlp.fc2.weight"])
         else:
             hidden = mamba2(W, c, i, xn, cache)
+        if c.mlp_width(i):                      # Block.mlp: norm2 + GatedMLP
+            xn, residual = add_norm(hidden, residual, W[p + "norm2.weight"], W.get(p + "norm2.bias"), c.eps, **kw)
+            y, gate = F.linear(xn, W[p + "mlp.fc1.weight"]).chunk(2, dim=-1)
+            hidden = F.linear(y * F.silu(gate), W[p + "mlp.fc2.weight"])
     s = hidden.float() + residual.float()
-    return F.layer_norm(s, (D,), W["backbone.norm_f.weight"].float(), W["backbone.norm_f.bias"].float(),
-                        c.eps).to(bf)
+    return norm(s, W["backbone.norm_f.weight"], W["backbone.norm_f.bias"], c.eps, c.rms_norm)

@@ -22,8 +22,25 @@ TINYH = HR.HybridCfg(d_model=256, n_layer=4, attn_layer_idx=(2,), n_heads=2, n_k
 def _engine(W, c=TINYH):
     from zonos_amd.hybrid import HybridDecoder, HybridEngineConfig
     ec = HybridEngineConfig(d_model=c.d_model, n_layer=c.n_layer, attn_layer_idx=c.attn_layer_idx, n_heads=c.n_heads,
-                            n_kv=c.n_kv, d_ff=c.d_ff, d_state=c.d_state, headdim=c.headdim, eps=c.eps)
+                            n_kv=c.n_kv, d_ff=c.d_ff, d_state=c.d_state, headdim=c.headdim, eps=c.eps, d_mlp=c.d_mlp,
+                            rms_norm=c.rms_norm, residual_in_fp32=c.residual_in_fp32)
     return HybridDecoder(ec, W, DEV)
+
+
+# The BackboneConfig variants the reference's mamba_ssm backbone honours (_mamba_ssm.py:18-31,49-57):
+# rms_norm, residual_in_fp32, an MLP on the Mamba2 blocks (d_intermediate != 0), and all three.
+# Parity with mamba_ssm unpinned (absent); pinned to the restatement's published semantics.
+VARIANTS = {
+    "rms": dict(rms_norm=True),
+    "fp32res": dict(residual_in_fp32=True),
+    "mamba_mlp": dict(d_mlp=384),
+    "all": dict(rms_norm=True, residual_in_fp32=True, d_mlp=256),
+}
+
+
+def _variant(name, base=None):
+    import dataclasses
+    return dataclasses.replace(base or TINYH, **VARIANTS[name])
 
 
 # one Mamba2 layer at the full hybrid widths (D 2048, d_inner 4096, d_state 128, headdim 64, 64 heads)
@@ -114,6 +131,121 @@ def test_hybrid_generate_teacher_forced_logits():
         worst = max(worst, float(e.max()))
         assert e.max() < 0.5 and e.mean() < 0.05, (s, e.max(), e.mean())
     print("hybrid teacher-forced logits: steps", n, "max abs err", worst)
+
+
+@pytest.mark.parametrize("name", list(VARIANTS))
+def test_hybrid_variant_teacher_forced_logits(name):
+    """the hybrid config variants run (no longer refused) and the whole generate() --
+    prefill, the graph-captured C decode step, the first block's own norm launch, the fp32 residual
+    stream, the Mamba-block MLP -- follows the restatement on its own greedy history: CFG logits within
+    the base hybrid test's bounds, tokens equal where the decision margin is clear."""
+    c = _variant(name)
+    W = HR.make_weights(c, seed=2, head_scale=4.0)
+    assert ("backbone.layers.0.norm.bias" in W) == (not c.rms_norm)
+    assert ("backbone.layers.0.mlp.fc1.weight" in W) == bool(c.d_mlp)
+    B, Lc, P, new = 3, 12, 4, 20
+    cond = zonos_ref.synthetic_conditioning(B, Lc, c.d_model)
+    prefix = zonos_ref.synthetic_prefix_codes(B, P)
+    sp = dict(temperature=0.0, top_p=0, top_k=0, min_p=0, linear=0, conf=0, quad=0, repetition_penalty=1.0,
+              repetition_penalty_window=2)
+    tr = {}
+    zonos_ref.generate(W, c, cond, prefix, new, 2.0, B, sp, seed=3, trace=tr)
+    gold = tr["delayed"]
+    eng = _engine(W, c)
+    assert eng.cfg.norm_flags == (2 if c.rms_norm else 0) | (4 if c.residual_in_fp32 else 0)
+    trace = {}
+
+    def force(frame, step):
+        off = P + 1 + step
+        if frame.shape[2]:
+            frame.copy_(gold[..., off:off + 1].to(frame.device))
+        return True
+
+    eng.generate(cond.to(DEV), prefix.to(DEV), new, 2.0, B, sp, seed=3, trace=trace,
+                 callback=lambda f, s_, n: force(f, s_), _after_prefill=lambda f: force(f, 0))
+    n = min(len(trace["logits"]), len(tr["logits"]))
+    assert n >= new // 2
+    worst, checked = 0.0, 0
+    for st in range(n):
+        ref = tr["logits"][st].float().numpy()
+        got = trace["logits"][st].cpu().numpy()
+        fin = np.isfinite(ref)
+        assert np.array_equal(fin, np.isfinite(got))
+        e = np.abs(got[fin] - ref[fin])
+        worst = max(worst, float(e.max()))
+        assert e.max() < 0.5 and e.mean() < 0.05, (name, st, e.max(), e.mean())
+        r = np.where(fin, ref, -np.inf).reshape(-1, ref.shape[-1])
+        g_ = np.where(fin, got, -np.inf).reshape(-1, ref.shape[-1])
+        top2 = np.sort(r, axis=-1)[:, -2:]
+        clear = (top2[:, 1] - top2[:, 0]) > 0.6
+        checked += int(clear.sum())
+        assert np.array_equal(r[clear].argmax(-1), g_[clear].argmax(-1)), (name, st)
+    print(f"hybrid variant {name}: steps {n}, max |d| {worst:.3f}, clear decisions checked {checked}")
+    assert checked > 0
+
+
+@pytest.mark.parametrize("name", ["fp32res", "all"])
+def test_c_hybrid_variant_step_equals_python_sequence(name, monkeypatch):
+    """The variants through the C ABI (zk_hybrid_prefill / zk_hybrid_decode_step with norm_flags, d_mlp,
+    xf) == the same sequence issued from Python, bit for bit, and the graph replay == eager."""
+    from zonos_amd.hybrid import HybridDecoder
+    c = _variant(name)
+    W = HR.make_weights(c, seed=7, head_scale=4.0)
+    eng = _engine(W, c)
+    B = 3
+    cond = zonos_ref.synthetic_conditioning(B, 12, c.d_model, seed=2).to(DEV)
+    prefix = zonos_ref.synthetic_prefix_codes(B, 3, seed=4).to(DEV)
+    sp = dict(temperature=1.0, top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
+              repetition_penalty_window=8)
+    outs = []
+    for flag in (True, False):
+        monkeypatch.setattr(HybridDecoder, "c_step", flag)
+        eng._ws = None
+        trace = {}
+        out = eng.generate(cond, prefix, 16, 2.0, B, sp, seed=9, trace=trace)
+        outs.append(([o.cpu() for o in out], [t.cpu() for t in trace["logits"]]))
+    (ca, la), (cb, lb) = outs
+    assert all(torch.equal(x, y) for x, y in zip(ca, cb)) and len(ca) == len(cb)
+    assert len(la) == len(lb) and all(torch.equal(x, y) for x, y in zip(la, lb))
+    monkeypatch.setattr(HybridDecoder, "c_step", True)
+    g = eng.generate(cond, prefix, 16, 2.0, B, sp, seed=9, poll_every=4)
+    assert all(torch.equal(x.cpu(), y) for x, y in zip(g, ca))
+
+
+def test_hybrid_variant_plugin_matches_oracle():
+    """HipHybridBackbone built from a BackboneConfig with all three variants (RMSNorm blocks without
+    bias parameters, fp32 residual, Mamba-block MLPs): state-dict names load unchanged and forward
+    (prefill + decodes) follows the restatement."""
+    from zonos.backbone import BACKBONES
+    from zonos_amd.config import BackboneConfig, InferenceParams
+    c = _variant("all")
+    W = HR.make_weights(c, seed=6)
+    bb = BACKBONES["mamba_ssm"](BackboneConfig(**c.to_zonos_config()["backbone"]))
+    sd = {k[len("backbone."):]: v for k, v in W.items() if k.startswith("backbone.")}
+    bb.load_state_dict(sd, strict=True)
+    bb = bb.to(DEV, torch.bfloat16)
+    R, S, n_dec = 4, 10, 4
+    g = torch.Generator().manual_seed(8)
+    xs = torch.randn(R, S + n_dec, c.d_model, generator=g).bfloat16()
+    ip = InferenceParams(max_seqlen=S + n_dec, max_batch_size=R,
+                         key_value_memory_dict=bb.allocate_inference_cache(R, S + n_dec),
+                         lengths_per_sample=torch.zeros(R, dtype=torch.int32))
+    cache = HR.HybridCache(c, R, S + n_dec)
+    rot = HR.rotary_table(16384, c.head_dim)
+    errs = []
+    for step in range(n_dec + 1):
+        sl = slice(0, S) if step == 0 else slice(S + step - 1, S + step)
+        got = bb(xs[:, sl].to(DEV), ip).float().cpu()
+        exp = HR.backbone(W, c, xs[:, sl], cache, rot).float()
+        nn_ = sl.stop - sl.start
+        ip.seqlen_offset += nn_
+        ip.lengths_per_sample += nn_
+        cache.seqlen_offset += nn_
+        cache.lengths += nn_
+        e = (got - exp).abs()
+        errs.append((float(e.max()), float(e.mean())))
+    print("hybrid variant plugin vs oracle |d| (max, mean) per call:", errs)
+    assert max(e[0] for e in errs) < 0.15 and max(e[1] for e in errs) < 0.015, errs
 
 
 @pytest.mark.parametrize("hp,ds,nh,R,gs,pos", [(32, 64, 16, 6, 2, 5), (64, 128, 64, 8, 2, 6), (64, 128, 64, 3, 1, 7),

@@ -50,7 +50,7 @@ class StepDesc(C.Structure):
 
 
 class HybridLayer(C.Structure):
-    _fields_ = [("type", C.c_int32), ("pad_", C.c_int32), ("ln1_w", P), ("ln1_b", P), ("wqkv", P), ("wo", P),
+    _fields_ = [("type", C.c_int32), ("d_mlp", C.c_int32), ("ln1_w", P), ("ln1_b", P), ("wqkv", P), ("wo", P),
                 ("ln2_w", P), ("ln2_b", P), ("fc1", P), ("fc2", P), ("k_cache", P), ("vt_cache", P), ("w_in", P),
                 ("conv_w", P), ("conv_b", P), ("A", P), ("dt_bias", P), ("Dskip", P), ("norm_w", P), ("w_out", P),
                 ("conv_state", P * 2), ("ssm_state", P * 2)]
@@ -60,10 +60,10 @@ class HybridDesc(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("B", "n_layer", "d_model", "n_heads", "n_kv", "head_dim", "d_ff", "smax",
                                          "d_inner", "nheads_ssm", "headdim_ssm", "d_state", "split_qkv", "split_o",
                                          "split_fc2", "split_heads", "split_inp", "split_out", "attn_splits",
-                                         "pad_")] + \
+                                         "norm_flags")] + \
               [("eps", F), ("gate_eps", F), ("layers", P), ("emb", P), ("heads", P), ("lnf_w", P), ("lnf_b", P),
                ("freqs", P), ("x", P), ("xn", P), ("y", P), ("h", P), ("part", P), ("attn_work", P), ("yz", P),
-               ("ym", P), ("xc", P), ("dbg", P), ("st", GenState), ("sp", SamplingParams)]
+               ("ym", P), ("xc", P), ("dbg", P), ("st", GenState), ("sp", SamplingParams), ("xf", P)]
 
 
 class DacResUnit(C.Structure):

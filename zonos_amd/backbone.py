@@ -43,10 +43,11 @@ class _Linear(nn.Module):
 
 
 class _LayerNorm(nn.Module):
-    def __init__(self, d):
+    def __init__(self, d, bias: bool = True):
         super().__init__()
         self.weight = nn.Parameter(torch.ones(d), requires_grad=False)
-        self.bias = nn.Parameter(torch.zeros(d), requires_grad=False)
+        if bias:                     # (mamba_ssm RMSNorm has no bias parameter)
+            self.bias = nn.Parameter(torch.zeros(d), requires_grad=False)
 
 
 class _Block(nn.Module):
@@ -182,22 +183,25 @@ class _Mamba2(nn.Module):
 
 
 class _HybridBlock(nn.Module):
-    """mamba_ssm Block names: norm + mixer (Mamba2 or MHA); attention blocks add norm2 + mlp."""
+    """mamba_ssm Block names: norm + mixer (Mamba2 or MHA); attention blocks add norm2 + mlp, and so do
+    Mamba2 blocks when d_intermediate != 0 (create_block); norms are bias-free RMSNorms under rms_norm."""
 
     def __init__(self, c: HybridEngineConfig, attn: bool):
         super().__init__()
         D = c.d_model
-        self.norm = _LayerNorm(D)
+        self.norm = _LayerNorm(D, bias=not c.rms_norm)
         if attn:
             self.mixer = nn.Module()
             self.mixer.in_proj = _Linear(D, (c.n_heads + 2 * c.n_kv) * c.head_dim)
             self.mixer.out_proj = _Linear(c.n_heads * c.head_dim, D)
-            self.norm2 = _LayerNorm(D)
-            self.mlp = nn.Module()
-            self.mlp.fc1 = _Linear(D, 2 * c.d_ff)
-            self.mlp.fc2 = _Linear(c.d_ff, D)
         else:
             self.mixer = _Mamba2(c)
+        width = c.d_ff if attn else c.d_mlp
+        if width:
+            self.norm2 = _LayerNorm(D, bias=not c.rms_norm)
+            self.mlp = nn.Module()
+            self.mlp.fc1 = _Linear(D, 2 * width)
+            self.mlp.fc2 = _Linear(width, D)
 
 
 def _has_ssm_layers(config: BackboneConfig) -> bool:
@@ -293,11 +297,14 @@ class HipHybridBackbone(HipZonosBackbone):
             splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R, target_blocks=128),
                           fc2=_split_for(D, max(Fd, 64), R), inp=1, out=_split_for(D, di, R))
         attn_splits = attn_splits_for(R, Hk, smax)
+        if c.d_mlp and not Fd and S == 1:
+            splits["fc2"] = _split_for(D, c.d_mlp, R)
         part_n = max(M * Nqkv * splits["qkv"], M * D * max(splits["o"], splits["fc2"], splits["out"]), M * nin)
         self._ws = dict(key=key, R=R, smax=smax, splits=splits, attn_splits=attn_splits,
                         x=torch.empty(M, D, dtype=bf, device=dev), xn=torch.empty(M, D, dtype=bf, device=dev),
+                        xf=torch.empty(M, D, dtype=f32, device=dev) if c.residual_in_fp32 else None,
                         q=torch.empty(M, H * hd, dtype=bf, device=dev), y=torch.empty(M, H * hd, dtype=bf, device=dev),
-                        h=torch.empty(M, max(Fd, 1), dtype=bf, device=dev),
+                        h=torch.empty(M, max(Fd, c.d_mlp, 1), dtype=bf, device=dev),
                         part=torch.empty(part_n, dtype=f32, device=dev),
                         yz=torch.empty(M, di, dtype=f32, device=dev), ym=torch.empty(M, di, dtype=bf, device=dev),
                         xc=torch.empty(M, c.conv_dim, dtype=bf, device=dev),
@@ -334,7 +341,11 @@ class HipHybridBackbone(HipZonosBackbone):
         M = R * S
         ws["x"].copy_(hidden_states.reshape(M, D))
         L0 = core.layers[0]
-        call("zk_layernorm", ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, M, D, ptr(ws["xn"]), stream)
+        if c.norm_flags:                            # rms_norm / residual_in_fp32: layer_norm_fn, residual None
+            core._prenorm(ws, M, stream, None)
+        else:
+            call("zk_layernorm", ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, M, D, ptr(ws["xn"]),
+                 stream)
         if S == 1:
             ws["scal"][1] = pos                     # position of the new token (ctx - 1; state parity)
         core._layers(ws, M, R, S, S > 1, stream, None)

@@ -28,20 +28,25 @@ namespace {
 // wv / bv: this thread's 8-element chunks of w and b, loaded by the caller before its own
 // loads complete (so they share the row's memory round trip); red: 2 * NT / 64 floats (one
 // partial-sum slot per wave for the mean and one for the variance: one barrier per reduction).
+// rms (block-uniform): RMS norm as mamba_ssm's layer_norm_fn(is_rms_norm=True) computes it -- no mean
+// (mean = 0, so x - mean = x and nb = -0.0: y = x * rstd * w + b exactly), var = sum(x^2) / D.
 template <int NT, int n8>
-ZK_DEV void ln_row_pre(const float* x, const uint4* wv, const uint4* bv, float eps, int D, bf16_t* y, float* red) {
+ZK_DEV void ln_row_pre(const float* x, const uint4* wv, const uint4* bv, float eps, int D, bf16_t* y, float* red,
+                       bool rms = false) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < n8; ++j)
-        if ((threadIdx.x + NT * j) * 8 < D)
-            for (int e = 0; e < 8; ++e) s += x[j * 8 + e];
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[w] = s;
-    __syncthreads();
     float t = 0.f;
+    if (!rms) {
+        float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < NT / 64; ++i) t += red[i];
+        for (int j = 0; j < n8; ++j)
+            if ((threadIdx.x + NT * j) * 8 < D)
+                for (int e = 0; e < 8; ++e) s += x[j * 8 + e];
+        s = wave_sum(s);
+        if ((threadIdx.x & 63) == 0) red[w] = s;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NT / 64; ++i) t += red[i];
+    }
     const float mean = t / (float)D;
     float v = 0.f;
 #pragma unroll
@@ -70,14 +75,15 @@ ZK_DEV void ln_row_pre(const float* x, const uint4* wv, const uint4* bv, float e
         *reinterpret_cast<uint4*>(y + c) = pack8(o);
     }
 }
-// the caller's w / b chunks (clamped index: unconditional loads stay in registers)
+// the caller's w / b chunks (clamped index: unconditional loads stay in registers). b == nullptr (a
+// bias-free RMSNorm): -0.0, the additive identity, so y = x_hat * w bit for bit.
 template <int NT, int n8>
 ZK_DEV void ln_load_wb(const bf16_t* w, const bf16_t* b, int D, uint4* wv, uint4* bv) {
 #pragma unroll
     for (int j = 0; j < n8; ++j) {
         const int c = min((int)(threadIdx.x + NT * j) * 8, D - 8);
         wv[j] = *reinterpret_cast<const uint4*>(w + c);
-        bv[j] = *reinterpret_cast<const uint4*>(b + c);
+        bv[j] = b ? *reinterpret_cast<const uint4*>(b + c) : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
     }
 }
 template <int NT, int n8>
@@ -219,6 +225,65 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln(const float* part, int nspli
         }
     }
     ln_row_pre<LN_NT, N8>(xv, wv, bv, eps, D, xn_out + (size_t)row * D, red);
+}
+
+// The hybrid backbone's config variants (mamba_ssm Block / layer_norm_fn with prenorm,
+// _mamba_ssm.py:18-31,49-57): flags bit 0 ln_on_sum (always set by the hybrid), bit 1 RMS norm
+// (is_rms_norm; b may be NULL for the bias-free block RMSNorm), bit 2 x_in fp32, bit 3 x_out fp32
+// (residual_in_fp32: the residual stream stays fp32 and hidden + residual is added in fp32);
+// nsplit 0 adds no projection (the first block's norm of the embedding: residual = hidden).
+// x_out = x_in + bf16(sum_s part[s]) in fp32 (rounded to bf16 unless bit 3); xn = norm of that fp32 sum.
+constexpr int RL_RMS = 2, RL_XIN32 = 4, RL_XOUT32 = 8;
+template <int N8>
+__global__ __launch_bounds__(LN_NT) void k_resid_ln_var(const float* part, int nsplit, const void* x_in,
+                                                        const bf16_t* w, const bf16_t* b, float eps, int rows, int D,
+                                                        void* x_out, bf16_t* xn_out, int flags, const int32_t* skip) {
+    __shared__ float red[2 * LN_NT / 64];
+    if (skip && *skip) return;
+    const int row = blockIdx.x;
+    const size_t slab = (size_t)rows * D;
+    uint4 wv[N8], bv[N8];
+    ln_load_wb<LN_NT, N8>(w, b, D, wv, bv);
+    float xv[N8 * 8];
+#pragma unroll
+    for (int j = 0; j < N8; ++j) {
+        const int c = (threadIdx.x + LN_NT * j) * 8;
+        if (c >= D) continue;
+        float xi[8];
+        if (flags & RL_XIN32) {
+            const float4* q = reinterpret_cast<const float4*>(static_cast<const float*>(x_in) + (size_t)row * D + c);
+            const float4 a = q[0], bb = q[1];
+            xi[0] = a.x; xi[1] = a.y; xi[2] = a.z; xi[3] = a.w; xi[4] = bb.x; xi[5] = bb.y; xi[6] = bb.z; xi[7] = bb.w;
+        } else {
+            unpack8(*reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(x_in) + (size_t)row * D + c), xi);
+        }
+        if (nsplit > 0) {
+            const float* p = part + (size_t)row * D + c;
+            float acc[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = p[e];
+            for (int sp = 1; sp < nsplit; ++sp)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] += p[sp * slab + e];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[j * 8 + e] = xi[e] + round_bf(acc[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[j * 8 + e] = xi[e];
+        }
+        if (flags & RL_XOUT32) {
+            float4* q = reinterpret_cast<float4*>(static_cast<float*>(x_out) + (size_t)row * D + c);
+            q[0] = make_float4(xv[j * 8], xv[j * 8 + 1], xv[j * 8 + 2], xv[j * 8 + 3]);
+            q[1] = make_float4(xv[j * 8 + 4], xv[j * 8 + 5], xv[j * 8 + 6], xv[j * 8 + 7]);
+        } else {
+            *reinterpret_cast<uint4*>(static_cast<bf16_t*>(x_out) + (size_t)row * D + c) = pack8(xv + 8 * j);
+            if (!(flags & 1)) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xv[j * 8 + e] = round_bf(xv[j * 8 + e]);
+            }
+        }
+    }
+    ln_row_pre<LN_NT, N8>(xv, wv, bv, eps, D, xn_out + (size_t)row * D, red, (flags & RL_RMS) != 0);
 }
 
 // k_resid_ln for D = 2048 with whole-line slab reads: 512 threads, thread t owns float4 piece t of
@@ -517,8 +582,20 @@ int zk_resid_ln_warm(const float* part, int nsplit, const void* x_in, const void
                      int rows, int D, void* x_out, void* xn_out, int ln_on_sum, const int32_t* skip, ZkWarm warm,
                      void* stream) {
     ZK_REQUIRE(D % 8 == 0 && D <= 8 * LN_NT * MAX_N8, "zk_resid_ln: unsupported D=%d", D);
-    ZK_REQUIRE(nsplit >= 1, "zk_resid_ln: nsplit must be >= 1");
+    ZK_REQUIRE(ln_on_sum >= 0 && ln_on_sum < 16, "zk_resid_ln: flags=%d", ln_on_sum);
+    ZK_REQUIRE(nsplit >= 1 || (nsplit == 0 && (ln_on_sum & 1)), "zk_resid_ln: nsplit must be >= 1 (0 with ln_on_sum)");
+    ZK_REQUIRE(nsplit == 0 || part != nullptr, "zk_resid_ln: part is NULL");
+    ZK_REQUIRE(b != nullptr || (ln_on_sum & RL_RMS), "zk_resid_ln: a LayerNorm needs its bias");
+    ZK_REQUIRE(x_in != nullptr && x_out != nullptr && w != nullptr && xn_out != nullptr, "zk_resid_ln: NULL buffer");
     if (rows == 0) return 0;
+    if (nsplit == 0 || (ln_on_sum & ~1)) {
+        // the hybrid variants (RMS norm, fp32 residual, no projection): rare configurations, one
+        // generic kernel; the default ln_on_sum paths below are untouched
+        ZK_LN_DISPATCH(D, k_resid_ln_var, dim3(rows), dim3(LN_NT), 0, (hipStream_t)stream, part, nsplit, x_in,
+                       (const bf16_t*)w, (const bf16_t*)b, eps, rows, D, x_out, (bf16_t*)xn_out, ln_on_sum, skip);
+        ZK_CHECK_LAUNCH("zk_resid_ln");
+        return 0;
+    }
     // D = 2048: 512-thread rows (8 slabs 4.27 vs 4.41 us with 256 threads x 2 pieces, c3 decode
     // step 3.635 vs 3.646 ms, profiles/r2_s4_resid_ln_512_ab.txt)
     if (D == 2048 && nsplit <= RL_MAXS) {

@@ -258,13 +258,34 @@ extern "C" int zk_prefill(const zk_step_desc* d, const void* cond, int Lc, int P
 namespace {
 bool hybrid_ok(const zk_hybrid_desc* d) {
     return d != nullptr && d->layers != nullptr && d->n_layer > 0 && d->B > 0 && d->d_inner > 0 &&
-           d->nheads_ssm * d->headdim_ssm == d->d_inner;
+           d->nheads_ssm * d->headdim_ssm == d->d_inner && (d->norm_flags & ~6) == 0;
 }
 
 // the block sequence of HybridDecoder._layers over M = R*S rows; prefill: S positions per row
+// norm_flags (zk_hybrid_desc): bit 1 rms_norm, bit 2 residual_in_fp32 -> zk_resid_ln flag words
+int hybrid_resid_flags(const zk_hybrid_desc* d) {
+    return 1 | (d->norm_flags & 2) | ((d->norm_flags & 4) ? (4 | 8) : 0);
+}
+void* hybrid_resid(const zk_hybrid_desc* d) { return (d->norm_flags & 4) ? d->xf : d->x; }
+
+// split-K of a GEMM with reduction length K: the requested split, lowered until it divides K into
+// 64-deep chunks (the Mamba-block MLP may be narrower than the attention MLP split_fc2 was chosen for)
+int fit_split(int K, int s) {
+    while (s > 1 && K % (s * 64) != 0) --s;
+    return s;
+}
+
+// the first block's norm of the embedding when the config variants are on (layer_norm_fn with
+// residual = None: residual = hidden, in fp32 under residual_in_fp32); x holds the embedding rows
+int hybrid_prenorm(const zk_hybrid_desc* d, int M, const int32_t* skip, void* stream) {
+    const int rf = 1 | (d->norm_flags & 2) | ((d->norm_flags & 4) ? 8 : 0);
+    return zk_resid_ln(nullptr, 0, d->x, d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, M, d->d_model,
+                       hybrid_resid(d), d->xn, rf, skip, stream);
+}
+
 int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, void* stream) {
     const int M = R * S;
-    const int D = d->d_model, H = d->n_heads, Hk = d->n_kv, hd = d->head_dim, Fd = d->d_ff;
+    const int D = d->d_model, H = d->n_heads, Hk = d->n_kv, hd = d->head_dim;
     const int Nqkv = (H + 2 * Hk) * hd, di = d->d_inner, nh = d->nheads_ssm;
     const int nin = 2 * di + 2 * d->d_state + nh;
     const int32_t* scal = d->st.scal;
@@ -273,10 +294,17 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
     const int sq = prefill ? 1 : d->split_qkv, so = prefill ? 1 : d->split_o, sf = prefill ? 1 : d->split_fc2;
     const int si = prefill ? 1 : d->split_inp, su = prefill ? 1 : d->split_out;
     const int K = d->st.K, V = d->st.V;
+    const int rf = hybrid_resid_flags(d);
+    void* xr = hybrid_resid(d);
+    if ((d->norm_flags & 4) && d->xf == nullptr) {
+        zk_set_error("zk_hybrid: residual_in_fp32 needs the fp32 residual buffer xf");
+        return -1;
+    }
+    const ZkWarm none{nullptr, 0, 0, 0, 0};
     // L2 warm-up (warm.h) of the GEMM that follows layer i's last k_resid_ln: the next layer's first
     // GEMM, or the heads
     auto next_warm = [&](int i) {
-        if (prefill) return ZkWarm{nullptr, 0, 0, 0, 0};
+        if (prefill) return none;
         if (i + 1 == d->n_layer) return warm_desc(d->heads, M, K * V, D, d->split_heads);
         const zk_hybrid_layer& N1 = d->layers[i + 1];
         return N1.type == 0 ? warm_desc(N1.wqkv, M, Nqkv, D, sq) : warm_desc(N1.w_in, M, nin, D, si);
@@ -286,6 +314,7 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
         const bool last = i + 1 == d->n_layer;
         const void* nw = last ? d->lnf_w : d->layers[i + 1].ln1_w;
         const void* nb = last ? d->lnf_b : d->layers[i + 1].ln1_b;
+        int smix;                               // split-K of the mixer's output projection
         if (L.type == 0) {
             ZK_STEP(zk_gemm_bf16(d->xn, D, L.wqkv, M, Nqkv, D, sq, 0, d->part, nullptr, skip, stream));
             if (prefill) {
@@ -297,13 +326,7 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
                                            pos, d->attn_work, d->attn_splits, d->y, 1, skip, stream));
             }
             ZK_STEP(zk_gemm_bf16(d->y, H * hd, L.wo, M, D, H * hd, so, 0, d->part, nullptr, skip, stream));
-            ZK_STEP(zk_resid_ln_warm(d->part, so, d->x, L.ln2_w, L.ln2_b, d->eps, M, D, d->x, d->xn, 1, skip,
-                                     prefill ? ZkWarm{nullptr, 0, 0, 0, 0} : warm_desc(L.fc1, M, 2 * Fd, D, 1, 1), stream));
-            ZK_STEP(zk_gemm_bf16_warm(d->xn, D, L.fc1, M, 2 * Fd, D, 1, 1, nullptr, d->h, skip,
-                                      prefill ? ZkWarm{nullptr, 0, 0, 0, 0} : warm_desc(L.fc2, M, D, Fd, sf), stream));
-            ZK_STEP(zk_gemm_bf16(d->h, Fd, L.fc2, M, D, Fd, sf, 0, d->part, nullptr, skip, stream));
-            ZK_STEP(zk_resid_ln_warm(d->part, sf, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, next_warm(i),
-                                     stream));
+            smix = so;
         } else if (L.type == 1) {
             ZK_STEP(zk_gemm_bf16(d->xn, D, L.w_in, M, nin, D, si, 0, d->part, nullptr, skip, stream));
             if (prefill) {
@@ -318,12 +341,24 @@ int hybrid_layers(const zk_hybrid_desc* d, int R, int S, bool prefill, void* q, 
             }
             ZK_STEP(zk_gated_rmsnorm(d->yz, M, di, L.norm_w, d->gate_eps, d->ym, skip, stream));
             ZK_STEP(zk_gemm_bf16(d->ym, di, L.w_out, M, D, di, su, 0, d->part, nullptr, skip, stream));
-            ZK_STEP(zk_resid_ln_warm(d->part, su, d->x, nw, nb, d->eps, M, D, d->x, d->xn, 1, skip, next_warm(i),
-                                     stream));
+            smix = su;
         } else {
             zk_set_error("zk_hybrid: layer %d has unknown type %d", i, L.type);
             return -1;
         }
+        // Block.mlp (_mamba_ssm.py:18-22: GatedMLP of d_intermediate on Mamba2 blocks when it is
+        // nonzero, of attn_mlp_d_intermediate on attention blocks): norm2 -> fc1 (SwiGLU) -> fc2
+        const int Fl = L.type == 0 ? (L.d_mlp > 0 ? L.d_mlp : d->d_ff) : L.d_mlp;
+        if (Fl > 0) {
+            const int sfl = prefill ? 1 : fit_split(Fl, sf);
+            ZK_STEP(zk_resid_ln_warm(d->part, smix, xr, L.ln2_w, L.ln2_b, d->eps, M, D, xr, d->xn, rf, skip,
+                                     prefill ? none : warm_desc(L.fc1, M, 2 * Fl, D, 1, 1), stream));
+            ZK_STEP(zk_gemm_bf16_warm(d->xn, D, L.fc1, M, 2 * Fl, D, 1, 1, nullptr, d->h, skip,
+                                      prefill ? none : warm_desc(L.fc2, M, D, Fl, sfl), stream));
+            ZK_STEP(zk_gemm_bf16(d->h, Fl, L.fc2, M, D, Fl, sfl, 0, d->part, nullptr, skip, stream));
+            smix = sfl;
+        }
+        ZK_STEP(zk_resid_ln_warm(d->part, smix, xr, nw, nb, d->eps, M, D, xr, d->xn, rf, skip, next_warm(i), stream));
     }
     return 0;
 }
@@ -337,8 +372,11 @@ extern "C" int zk_hybrid_decode_step(const zk_hybrid_desc* d, void* stream) {
     const int K = d->st.K, V = d->st.V, B = d->B, R = 2 * B, D = d->d_model;
     int32_t* scal = d->st.scal;
     const int32_t* skip = scal + 3;
+    const bool var = (d->norm_flags & 6) != 0;       // config variants: the first norm is its own launch
     ZK_STEP(zk_embed_codes(d->st.delayed, B, 1, K, (long)d->st.Ld * K, d->st.Ld, scal, -1, d->emb, V, D, 2, d->x, 1, 0,
-                           d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, d->xn, skip, stream));
+                           var ? nullptr : d->layers[0].ln1_w, var ? nullptr : d->layers[0].ln1_b, d->eps,
+                           var ? nullptr : d->xn, skip, stream));
+    if (var) ZK_STEP(hybrid_prenorm(d, R, skip, stream));
     ZK_STEP(hybrid_layers(d, R, 1, false, nullptr, stream));
     ZK_STEP(zk_gemm_bf16(d->xn, D, d->heads, R, K * V, D, d->split_heads, 0, d->part, nullptr, skip, stream));
     ZK_STEP(zk_sample_heads(d->part, d->split_heads, &d->st, &d->sp, 0, 0, d->dbg, stream));
@@ -368,7 +406,8 @@ extern "C" int zk_hybrid_prefill(const zk_hybrid_desc* d, const void* cond, int 
     }
     ZK_STEP(zk_embed_codes(d->st.delayed, B, P + 1, K, (long)d->st.Ld * K, d->st.Ld, nullptr, 0, d->emb, V, D, 2,
                            d->x, S, Lc, nullptr, nullptr, d->eps, nullptr, nullptr, stream));
-    ZK_STEP(zk_layernorm(d->x, d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, R * S, D, d->xn, stream));
+    if (d->norm_flags & 6) ZK_STEP(hybrid_prenorm(d, R * S, nullptr, stream));
+    else ZK_STEP(zk_layernorm(d->x, d->layers[0].ln1_w, d->layers[0].ln1_b, d->eps, R * S, D, d->xn, stream));
     ZK_STEP(hybrid_layers(d, R, S, true, q, stream));
     ZK_STEP(zk_gemm_bf16(static_cast<const char*>(d->xn) + (size_t)(S - 1) * row, (long)S * D, d->heads, R, K * V, D,
                          d->split_heads, 0, d->part, nullptr, nullptr, stream));

@@ -234,6 +234,9 @@ class HipDecoder(HipBackbone):
     # B <= 8 decode (R <= 16 rows) runs each block as five launches (zk_gemv_fused: LayerNorm
     # prologues, residual epilogues, no split-K slabs) instead of seven
     small_batch_path = True
+    # layer 0's norm is fused into the embedding kernel (decode) / a zk_layernorm (prefill); False:
+    # the subclass runs it as _prenorm (the hybrid backbone's RMS-norm / fp32-residual variants)
+    embed_norm = True
 
     def __init__(self, cfg: EngineConfig, weights: dict, device="cuda"):
         super().__init__(cfg, weights, device)
@@ -370,9 +373,12 @@ class HipDecoder(HipBackbone):
         skip = ptr(scal[3:4])
         L0 = self.layers[0]
         small = self._small(R)                       # layer 0's LayerNorm runs in the in_proj prologue
+        own = small or not self.embed_norm           # ... or its own launch (hybrid config variants)
         call("zk_embed_codes", ptr(ws["delayed"]), B, 1, N_CB, ws["Ld"] * N_CB, ws["Ld"], ptr(scal[0:1]), -1,
-             ptr(self.emb), VOCAB, c.d_model, 2, ptr(ws["x"]), 1, 0, None if small else ptr(L0["ln1_w"]),
-             None if small else ptr(L0["ln1_b"]), c.eps, None if small else ptr(ws["xn"]), skip, stream)
+             ptr(self.emb), VOCAB, c.d_model, 2, ptr(ws["x"]), 1, 0, None if own else ptr(L0["ln1_w"]),
+             None if own else ptr(L0["ln1_b"]), c.eps, None if own else ptr(ws["xn"]), skip, stream)
+        if not self.embed_norm:
+            self._prenorm(ws, R, stream, skip)
         logits, nsp = ws["part"], ws["splits"]["heads"]
         if small:
             self._layers_small(ws, R, stream, skip)
@@ -443,8 +449,11 @@ class HipDecoder(HipBackbone):
             call("zk_embed_codes", ptr(ws["delayed"]), B, P + 1, N_CB, Ld * N_CB, Ld, None, 0, ptr(self.emb), VOCAB,
                  D, 2, ptr(ws["x"]), S, Lc, None, None, c.eps, None, None, stream)
             L0 = self.layers[0]
-            call("zk_layernorm", ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, R * S, D, ptr(ws["xn"]),
-                 stream)
+            if self.embed_norm:
+                call("zk_layernorm", ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, R * S, D,
+                     ptr(ws["xn"]), stream)
+            else:
+                self._prenorm(ws, R * S, stream, None)
             self._layers(ws, R * S, R, S, True, stream, None)
             self._heads(ws, R, S, stream, None)
             call("zk_sample_heads", ptr(ws["part"]), ws["splits"]["heads"], C_ref(st), C_ref(sp), 1, 0,

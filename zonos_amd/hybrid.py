@@ -43,6 +43,19 @@ class HybridEngineConfig:
     ngroups: int = 1
     rotary_base: float = 10000.0
     eps: float = 1e-5
+    d_mlp: int = 0                   # GatedMLP width of the Mamba2 blocks (BackboneConfig.d_intermediate; 0: none)
+    rms_norm: bool = False           # block norms RMSNorm (bias-free), norm_f an RMS norm (with its bias)
+    residual_in_fp32: bool = False   # residual stream kept in fp32
+
+    @property
+    def norm_flags(self) -> int:
+        """zk_hybrid_desc.norm_flags: bit 1 rms_norm, bit 2 residual_in_fp32."""
+        return (2 if self.rms_norm else 0) | (4 if self.residual_in_fp32 else 0)
+
+    @property
+    def resid_flags(self) -> int:
+        """zk_resid_ln flag word of every block-boundary add + norm (include/zonos_hip.h)."""
+        return 1 | (2 if self.rms_norm else 0) | (12 if self.residual_in_fp32 else 0)
 
     @property
     def head_dim(self):
@@ -76,15 +89,22 @@ class HybridEngineConfig:
             raise ValueError("biased attention projections are not supported")
         if a.get("rotary_emb_interleaved", False):
             raise ValueError("interleaved rotary embeddings are not supported (GPT-NeoX rotate-half only)")
-        if (has_ssm and bc.d_intermediate != 0) or bc.rms_norm or bc.residual_in_fp32:
-            raise ValueError("hybrid variant not supported (d_intermediate / rms_norm / residual_in_fp32)")
         if a.get("rotary_emb_dim", bc.d_model // a.get("num_heads", 16)) != bc.d_model // a.get("num_heads", 16):
             raise ValueError("partial rotary embeddings are not supported")
+
+        def gated_width(n):          # mamba_ssm GatedMLP: hidden_features rounded up to multiple_of = 128
+            return (n + 127) // 128 * 128 if n else 0
+
+        # create_block (_mamba_ssm.py:18-31): Mamba2 blocks get GatedMLP(d_intermediate) when it is
+        # nonzero, attention blocks GatedMLP(attn_mlp_d_intermediate); rms_norm / residual_in_fp32
+        # go to every Block and to the final layer_norm_fn (:49-57)
         return cls(d_model=bc.d_model, n_layer=bc.n_layer, attn_layer_idx=tuple(bc.attn_layer_idx),
                    n_heads=a.get("num_heads", 16), n_kv=a.get("num_heads_kv", a.get("num_heads", 16)),
-                   d_ff=bc.attn_mlp_d_intermediate, d_state=s.get("d_state", 128), d_conv=s.get("d_conv", 4),
-                   expand=s.get("expand", 2), headdim=s.get("headdim", 64), ngroups=s.get("ngroups", 1),
-                   rotary_base=a.get("rotary_emb_base", 10000.0), eps=bc.norm_epsilon)
+                   d_ff=gated_width(bc.attn_mlp_d_intermediate), d_state=s.get("d_state", 128),
+                   d_conv=s.get("d_conv", 4), expand=s.get("expand", 2), headdim=s.get("headdim", 64),
+                   ngroups=s.get("ngroups", 1), rotary_base=a.get("rotary_emb_base", 10000.0), eps=bc.norm_epsilon,
+                   d_mlp=gated_width(bc.d_intermediate) if has_ssm else 0, rms_norm=bool(bc.rms_norm),
+                   residual_in_fp32=bool(bc.residual_in_fp32))
 
 
 def rotary_table(seq_len: int, dim: int, base: float = 10000.0) -> torch.Tensor:
@@ -118,19 +138,26 @@ class HybridBackbone:
         def f32(name):
             return weights[prefix + name].to(device=dev, dtype=bf).float().contiguous()
 
+        def wb(name):                # a norm bias: absent from a bias-free RMSNorm (rms_norm)
+            return None if cfg.rms_norm else w(name)
+
+        def mlp(p, width):           # norm2 + GatedMLP (fc1 rows interleaved for the SwiGLU epilogue)
+            fc1 = w(p + "mlp.fc1.weight")
+            if fc1.shape[0] != 2 * width:
+                raise ValueError(f"{p}mlp.fc1.weight has {fc1.shape[0]} rows, the config says 2 x {width}")
+            fc1p = torch.empty_like(fc1)
+            call("zk_permute_fc1", ptr(fc1), width, cfg.d_model, ptr(fc1p), stream)
+            return dict(ln2_w=w(p + "norm2.weight"), ln2_b=wb(p + "norm2.bias"), d_mlp=width,
+                        fc1=pack_weights(fc1p, stream), fc2=pack_weights(w(p + "mlp.fc2.weight"), stream))
+
         stream = _lib.stream_ptr(dev)
         self.layers = []
         for i in range(cfg.n_layer):
             p = f"layers.{i}."
-            L = dict(ln1_w=w(p + "norm.weight"), ln1_b=w(p + "norm.bias"))
+            L = dict(ln1_w=w(p + "norm.weight"), ln1_b=wb(p + "norm.bias"), d_mlp=0)
             if i in cfg.attn_layer_idx:
-                fc1 = w(p + "mlp.fc1.weight")
-                fc1p = torch.empty_like(fc1)
-                call("zk_permute_fc1", ptr(fc1), cfg.d_ff, cfg.d_model, ptr(fc1p), stream)
                 L.update(type="attn", wqkv=pack_weights(w(p + "mixer.in_proj.weight"), stream),
-                         wo=pack_weights(w(p + "mixer.out_proj.weight"), stream),
-                         ln2_w=w(p + "norm2.weight"), ln2_b=w(p + "norm2.bias"),
-                         fc1=pack_weights(fc1p, stream), fc2=pack_weights(w(p + "mlp.fc2.weight"), stream))
+                         wo=pack_weights(w(p + "mixer.out_proj.weight"), stream), **mlp(p, cfg.d_ff))
             else:
                 cw = weights[prefix + p + "mixer.conv1d.weight"].to(device=dev, dtype=bf).float()
                 L.update(type="mamba", w_in=pack_weights(w(p + "mixer.in_proj.weight"), stream),
@@ -140,6 +167,8 @@ class HybridBackbone:
                          dt_bias=f32(p + "mixer.dt_bias"), D=f32(p + "mixer.D"),
                          norm_w=f32(p + "mixer.norm.weight"),
                          w_out=pack_weights(w(p + "mixer.out_proj.weight"), stream))
+                if cfg.d_mlp:
+                    L.update(mlp(p, cfg.d_mlp))
             self.layers.append(L)
         self.attn_ids = [i for i in range(cfg.n_layer) if i in cfg.attn_layer_idx]
         self.mamba_ids = [i for i in range(cfg.n_layer) if i not in cfg.attn_layer_idx]
@@ -169,6 +198,8 @@ class HybridBackbone:
         Nqkv = (H + 2 * Hk) * hd
         sp = ws["splits"] if not prefill else dict(qkv=1, o=1, fc2=1, inp=1, out=1)
         x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
+        xr = ws["xf"] if c.residual_in_fp32 else x           # the residual stream
+        rf = c.resid_flags
         scal = ws["scal"]
         pos_dev = None if prefill else ptr(scal[1:2])
         for i, L in enumerate(self.layers):
@@ -176,6 +207,10 @@ class HybridBackbone:
                 nw, nb = self.layers[i + 1]["ln1_w"], self.layers[i + 1]["ln1_b"]
             else:
                 nw, nb = self.lnf_w, self.lnf_b
+            if c.norm_flags or c.d_mlp:
+                # the same sequence as zk_hybrid_decode_step's (capi.cpp hybrid_layers) for the variants
+                self._layer_var(ws, i, L, M, R, S, prefill, stream, skip, sp, xr, rf, nw, nb, pos_dev)
+                continue
             if L["type"] == "attn":
                 kc, vt = self._kv(ws, i)
                 call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip,
@@ -220,6 +255,68 @@ class HybridBackbone:
                      skip, stream)
 
 
+    def _layer_var(self, ws, i, L, M, R, S, prefill, stream, skip, sp, xr, rf, nw, nb, pos_dev):
+        """One block under rms_norm / residual_in_fp32 / a Mamba-block MLP (capi.cpp hybrid_layers)."""
+        c = self.cfg
+        D, H, Hk, hd = c.d_model, c.n_heads, c.n_kv, c.head_dim
+        di, nin, nh = c.d_inner, c.d_in_proj, c.nheads_ssm
+        Nqkv = (H + 2 * Hk) * hd
+        xn, q, y, h, part = ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
+        if L["type"] == "attn":
+            kc, vt = self._kv(ws, i)
+            call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
+            if prefill:
+                call("zk_qkv_rope", ptr(part), 1, R, S, H, Hk, hd, ptr(self.freqs), 0, None, ptr(q), ptr(kc), ptr(vt),
+                     ws["smax"], None, 1, skip, stream)
+                call("zk_attn_prefill", ptr(q), ptr(kc), ptr(vt), R, S, H, Hk, hd, ws["smax"], ptr(y), stream)
+            else:
+                call("zk_attn_decode_qkv", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
+                     ws["smax"], 1, pos_dev, ptr(ws["attn_work"]), ws["attn_splits"], ptr(y), 1, skip, stream)
+            call("zk_gemm_bf16", ptr(y), H * hd, ptr(L["wo"]), M, D, H * hd, sp["o"], 0, ptr(part), None, skip, stream)
+            smix = sp["o"]
+        else:
+            conv, ssm = self._states(ws, i)
+            call("zk_gemm_bf16", ptr(xn), D, ptr(L["w_in"]), M, nin, D, sp["inp"], 0, ptr(part), None, skip, stream)
+            if prefill:
+                call("zk_mamba_prefill", ptr(part), R, S, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
+                     ptr(L["conv_b"]), ptr(ws["xc"]), ptr(conv[S & 1]), ptr(ssm[S & 1]), ptr(L["A"]),
+                     ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), stream)
+            else:
+                call("zk_mamba_step", ptr(part), sp["inp"], R, di, nh, c.headdim, c.d_state, ptr(L["conv_w"]),
+                     ptr(L["conv_b"]), ptr(conv[0]), ptr(conv[1]), pos_dev, ptr(ssm[0]), ptr(ssm[1]), ptr(L["A"]),
+                     ptr(L["dt_bias"]), ptr(L["D"]), ptr(ws["yz"]), skip, stream)
+            call("zk_gated_rmsnorm", ptr(ws["yz"]), M, di, ptr(L["norm_w"]), 1e-5, ptr(ws["ym"]), skip, stream)
+            call("zk_gemm_bf16", ptr(ws["ym"]), di, ptr(L["w_out"]), M, D, di, sp["out"], 0, ptr(part), None, skip,
+                 stream)
+            smix = sp["out"]
+        Fl = L["d_mlp"]
+        if Fl:
+            sfl = fit_split(Fl, sp["fc2"])
+            call("zk_resid_ln", ptr(part), smix, ptr(xr), ptr(L["ln2_w"]), ptr(L["ln2_b"]), c.eps, M, D, ptr(xr),
+                 ptr(xn), rf, skip, stream)
+            call("zk_gemm_bf16", ptr(xn), D, ptr(L["fc1"]), M, 2 * Fl, D, 1, 1, None, ptr(h), skip, stream)
+            call("zk_gemm_bf16", ptr(h), Fl, ptr(L["fc2"]), M, D, Fl, sfl, 0, ptr(part), None, skip, stream)
+            smix = sfl
+        call("zk_resid_ln", ptr(part), smix, ptr(xr), ptr(nw), ptr(nb), c.eps, M, D, ptr(xr), ptr(xn), rf, skip,
+             stream)
+
+    def _prenorm(self, ws, M: int, stream, skip):
+        """The first block's norm of the embedding rows in ws["x"] under the config variants
+        (layer_norm_fn with residual = None; capi.cpp hybrid_prenorm)."""
+        c = self.cfg
+        L0 = self.layers[0]
+        xr = ws["xf"] if c.residual_in_fp32 else ws["x"]
+        call("zk_resid_ln", None, 0, ptr(ws["x"]), ptr(L0["ln1_w"]), ptr(L0["ln1_b"]), c.eps, M, c.d_model, ptr(xr),
+             ptr(ws["xn"]), 1 | (2 if c.rms_norm else 0) | (8 if c.residual_in_fp32 else 0), skip, stream)
+
+
+def fit_split(K: int, s: int) -> int:
+    """capi.cpp fit_split: the requested split-K, lowered until it divides K into 64-deep chunks."""
+    while s > 1 and K % (s * 64):
+        s -= 1
+    return s
+
+
 class HybridDecoder(HybridBackbone, HipDecoder):
     """generate() for the hybrid backbone (the layer loop and state differ from HipDecoder)."""
 
@@ -230,6 +327,7 @@ class HybridDecoder(HybridBackbone, HipDecoder):
 
     def __init__(self, cfg: HybridEngineConfig, weights: dict, device="cuda"):
         HybridBackbone.__init__(self, cfg, weights, device)
+        self.embed_norm = not cfg.norm_flags
         dev, bf = self.device, torch.bfloat16
 
         def w(name):
@@ -279,6 +377,9 @@ class HybridDecoder(HybridBackbone, HipDecoder):
                       fc2=_split_for(D, max(Fd, 64), R), heads=1, inp=1, out=_split_for(D, di, R))
         part_n = max(Mp * Nqkv, Mp * D, Mp * nin, splits["qkv"] * R * Nqkv, splits["o"] * R * D,
                      splits["fc2"] * R * D, splits["heads"] * R * Nh, splits["inp"] * R * nin, splits["out"] * R * D)
+        if c.d_mlp and not Fd:       # a Mamba-block MLP without attention MLPs: its own fc2 split
+            splits["fc2"] = _split_for(D, c.d_mlp, R)
+            part_n = max(part_n, splits["fc2"] * R * D)
         attn_splits = attn_splits_for(R, Hk, smax)
         na, nm = len(self.attn_ids), len(self.mamba_ids)
         ws = dict(
@@ -289,7 +390,8 @@ class HybridDecoder(HybridBackbone, HipDecoder):
             ssm=torch.zeros(max(nm, 1), 2, R * c.nheads_ssm * c.headdim * c.d_state, dtype=bf, device=dev),
             x=torch.empty(Mp, D, dtype=bf, device=dev), xn=torch.empty(Mp, D, dtype=bf, device=dev),
             q=torch.empty(Mp, H * hd, dtype=bf, device=dev), y=torch.empty(Mp, H * hd, dtype=bf, device=dev),
-            h=torch.empty(Mp, max(Fd, 1), dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
+            h=torch.empty(Mp, max(Fd, c.d_mlp, 1), dtype=bf, device=dev), part=torch.empty(part_n, dtype=f32, device=dev),
+            xf=torch.empty(Mp, D, dtype=f32, device=dev) if c.residual_in_fp32 else None,
             yz=torch.empty(Mp, di, dtype=f32, device=dev), ym=torch.empty(Mp, di, dtype=bf, device=dev),
             xc=torch.empty(Mp, c.conv_dim, dtype=bf, device=dev),
             attn_work=torch.empty(max(1, R * Hk * attn_splits * (8 + 4 * hd)), dtype=f32, device=dev),
@@ -314,6 +416,9 @@ class HybridDecoder(HybridBackbone, HipDecoder):
             for i, L in enumerate(self.layers):
                 e = _lib.HybridLayer()
                 e.ln1_w, e.ln1_b = ptr(L["ln1_w"]), ptr(L["ln1_b"])
+                e.d_mlp = L["d_mlp"] if L["type"] != "attn" else 0
+                if L["d_mlp"]:
+                    e.ln2_w, e.ln2_b, e.fc1, e.fc2 = ptr(L["ln2_w"]), ptr(L["ln2_b"]), ptr(L["fc1"]), ptr(L["fc2"])
                 if L["type"] == "attn":
                     kc, vt = self._kv(ws, i)
                     e.type = 0
@@ -332,11 +437,11 @@ class HybridDecoder(HybridBackbone, HipDecoder):
         sps = ws["splits"]
         return _lib.HybridDesc(B, c.n_layer, c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff, ws["smax"],
                                c.d_inner, c.nheads_ssm, c.headdim, c.d_state, sps["qkv"], sps["o"], sps["fc2"],
-                               sps["heads"], sps["inp"], sps["out"], ws["attn_splits"], 0, c.eps, 1e-5,
+                               sps["heads"], sps["inp"], sps["out"], ws["attn_splits"], c.norm_flags, c.eps, 1e-5,
                                C.cast(ws["hybrid_layers"], C.c_void_p), ptr(self.emb), ptr(self.heads),
                                ptr(self.lnf_w), ptr(self.lnf_b), ptr(self.freqs), ptr(ws["x"]), ptr(ws["xn"]),
                                ptr(ws["y"]), ptr(ws["h"]), ptr(ws["part"]), ptr(ws["attn_work"]), ptr(ws["yz"]),
-                               ptr(ws["ym"]), ptr(ws["xc"]), ptr(ws["dbg"]), st, sp)
+                               ptr(ws["ym"]), ptr(ws["xc"]), ptr(ws["dbg"]), st, sp, ptr(ws["xf"]))
 
     def _c_decode(self, ws, B, st, sp, stream):
         call("zk_hybrid_decode_step", C.byref(self._step_desc(ws, B, st, sp)), stream)
