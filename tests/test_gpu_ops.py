@@ -123,6 +123,37 @@ def test_gemm_narrow_wide_workgroups_bit_identical(N, N2, nsplit):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,K", [(16400, 4096, 1024), (8300, 2112, 512)])
+def test_prefill_gemm_epilogues_consistent(M, N, K):
+    """k_gemm_pf's LDS-staged epilogues (whole-row stores, round 5): the SwiGLU output of mode 1 is
+    the SwiGLU of mode 0's fp32 output over the same interleaved weights (both modes accumulate in one
+    K order), computed here with torch: equal except where expf and torch.exp round the silu
+    differently (<= 1 bf16 ulp of the product on a few elements); mode 0 against an fp32 reference."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import pack_weights
+    g = torch.Generator(device="cpu").manual_seed(M)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    s = stream_ptr()
+    Wp = torch.empty_like(W)
+    call("zk_permute_fc1", ptr(W), N // 2, K, ptr(Wp), s)
+    Wpk = pack_weights(Wp, s)
+    C = torch.empty(M, N, device=DEV)
+    call("zk_gemm_bf16", ptr(A), K, ptr(Wpk), M, N, K, 1, 0, ptr(C), None, None, s)
+    ref = A.float() @ Wp.float().t()
+    assert torch.allclose(C, ref, atol=2e-3 * (K / 2048) ** 0.5, rtol=1e-3), (C - ref).abs().max()
+    h = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+    call("zk_gemm_bf16", ptr(A), K, ptr(Wpk), M, N, K, 1, 1, None, ptr(h), None, s)
+    Cq = C.view(M, N // 16, 2, 8)
+    y, gt = Cq[:, :, 0].bfloat16().float(), Cq[:, :, 1].bfloat16().float()
+    sl = (gt / (1.0 + torch.exp(-gt))).bfloat16().float()
+    exp = (y * sl).bfloat16().reshape(M, N // 2)
+    d = (h.float() - exp.float()).abs()
+    ulp = exp.float().abs().clamp_min(1e-30) * 2 ** -7
+    assert bool((d <= ulp * 1.01).all()), float((d / ulp).max())
+    assert float((d > 0).float().mean()) < 1e-3
+
+
 def test_pack_weights_layout():
     """Fragment-packed layout: block (nt, kc) lane l holds W[16nt + l%16][32kc + 8(l//16) .. +8]."""
     from zonos_amd._lib import stream_ptr

@@ -24,6 +24,9 @@
 namespace {
 
 constexpr int PF_BM = 256, PF_BN = 256, PF_NT = 512;
+#ifndef ZK_PF_EPI
+#define ZK_PF_EPI 1                        // LDS-staged whole-row epilogues (0: direct register stores, A/B)
+#endif
 
 // Activation rows in LDS: BKS-deep steps give rows of 2 * BKS bytes. The 16-B chunk c of row r is
 // stored at chunk c ^ swz(r), which makes every ds_read_b128 of an A fragment (16 rows x one chunk
@@ -101,6 +104,81 @@ ZK_DEV void pf_epilogue(const f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc
                         Cb[(size_t)m * F + f] = f2bf(mine * sl);
                     }
                 }
+        }
+    }
+}
+
+// Epilogues staged through the (then idle) LDS stages, so every global store writes whole rows:
+// the register layout above writes 16 columns of 4 rows per instruction (64-B fp32 pieces, or 16-B
+// bf16 pieces from half the lanes in the SwiGLU form).
+//   mode 1: the bf16-rounded y / gate columns of the whole 256 x 256 tile (row stride PF_ES halves,
+//           padded against bank conflicts), then every lane computes y * silu(gate) for 8 outputs
+//           and stores them as one 16-B piece: 16 lanes write a 256-B row segment (the arithmetic and
+//           rounding points of pf_epilogue<1>, bit-identical);
+//   mode 0: the fp32 tile in two halves of 128 rows (row stride PF_EF floats), each stored as whole
+//           1 KB rows (one wave instruction per row).
+constexpr int PF_ES = PF_BN + 8;                   // mode 1 staging row stride (halves)
+constexpr int PF_EF = PF_BN + 4;                   // mode 0 staging row stride (floats)
+constexpr int PF_EPI_LDS1 = PF_BM * PF_ES * 2;     // 135,168 B
+constexpr int PF_EPI_LDS0 = (PF_BM / 2) * PF_EF * 4;   // 133,120 B
+template <int MODE>
+ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][4], char* smem, int m0, int n0, int wr, int wc, int ln, int lg,
+                            int M, int N, float* __restrict__ C, bf16_t* __restrict__ Cb) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();                                   // every wave's last stage read
+    if constexpr (MODE == 1) {
+        bf16_t* t = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    t[(wr * 128 + mt * 16 + lg * 4 + i) * PF_ES + wc * 64 + nt * 16 + ln] = f2bf(acc[mt][nt][i]);
+        __syncthreads();
+        const int F = N / 2, f0 = n0 / 2;
+        const int gi = tid & 15;                       // 16-column group of the row: outputs f0 + 8 gi ..
+#pragma unroll
+        for (int it = 0; it < PF_BM / 32; ++it) {
+            const int r = it * 32 + (tid >> 4), m = m0 + r;
+            if (m >= M || f0 + gi * 8 >= F) continue;
+            const bf16_t* src = t + r * PF_ES + gi * 16;
+            const uint4 yv = *reinterpret_cast<const uint4*>(src), gv = *reinterpret_cast<const uint4*>(src + 8);
+            float y[8], g[8], o[8];
+            unpack8(yv, y);
+            unpack8(gv, g);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float sl = round_bf(g[j] / (1.0f + expf(-g[j])));     // F.silu in bf16
+                o[j] = y[j] * sl;
+            }
+            *reinterpret_cast<uint4*>(Cb + (size_t)m * F + f0 + gi * 8) = pack8(o);
+        }
+    } else {
+        float* t = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            if (wr == half) {
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            t[(mt * 16 + lg * 4 + i) * PF_EF + wc * 64 + nt * 16 + ln] = acc[mt][nt][i];
+            }
+            __syncthreads();
+            // 128 rows x 1 KB: wave w stores rows w, w + 8, ...; lane L the floats 4L .. 4L + 3
+#pragma unroll 4
+            for (int r = w; r < 128; r += 8) {
+                const int m = m0 + half * 128 + r;
+                if (m < M && n0 + 4 * lane < N) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(t + r * PF_EF + 4 * lane);
+                    *reinterpret_cast<f32x4*>(C + (size_t)m * N + n0 + 4 * lane) = v;
+                }
+            }
+            if (half == 0) __syncthreads();            // the second half overwrites the staging rows
         }
     }
 }
@@ -202,7 +280,8 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
         }
     }
 
-    pf_epilogue<MODE>(acc, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
+    if (ZK_PF_EPI && (MODE == 1 || N % 4 == 0)) pf_epilogue_lds<MODE>(acc, smem, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
+    else pf_epilogue<MODE>(acc, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
 }
 
 }  // namespace
@@ -221,7 +300,9 @@ bool zk_gemm_pf_applies(int M, int N, int K, int nsplit) {
 #define ZK_PF_BKS 64
 #endif
 constexpr int PF_BKS = ZK_PF_BKS, PF_NSTG = PF_BKS == 64 ? 2 : 4;
-constexpr int PF_LDS = PF_NSTG * (PF_BM + PF_BN) * PF_BKS * 2;
+constexpr int PF_LDS_MAIN = PF_NSTG * (PF_BM + PF_BN) * PF_BKS * 2;
+constexpr int pf_max(int a, int b) { return a > b ? a : b; }
+constexpr int PF_LDS = pf_max(PF_LDS_MAIN, ZK_PF_EPI ? pf_max(PF_EPI_LDS1, PF_EPI_LDS0) : 0);
 
 int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int mode, float* C, void* Cb,
                const int32_t* skip, void* stream) {
