@@ -1,0 +1,9 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r5_fuse
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -q --timeout 120 --timeout-method thread -k "resid or gemm_ln" > $O/t.log 2>&1
+rc=$?; tail -n 3 $O/t.log; grep -E "^E |Error|FAILED" $O/t.log | head -20
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 180 python tools/microbench.py resid 2>&1 | grep -v amdgpu
+timeout -k 10 400 python -u tools/fuse_ab.py 512 2 2>&1 | grep -v amdgpu
