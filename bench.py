@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=1)
     ap.add_argument("--stub", action="store_true", help="CPU stand-in workload (launcher/reporting tests)")
+    ap.add_argument("--graph-steps", type=int, default=None,
+                    help="decode steps per hipGraph replay (default: the engine's graph_steps)")
     return ap.parse_args()
 
 
@@ -374,6 +376,8 @@ class GpuWorkload:
             W = synthetic.backbone_weights(dev, seed=0, **mc)
             self.eng = HipDecoder(EngineConfig(**mc), W, dev)
         del W
+        if args.graph_steps:
+            self.eng.graph_steps = args.graph_steps
         self.mc = mc
         self.dac = None if args.no_dac else HipDacDecoder(DacSpec(), synthetic.dac_weights(dev), dev)
         B = args.batch

@@ -99,26 +99,6 @@ int zk_resid_ln(const float* part, int nsplit, const void* x_in, const void* w, 
  * W is in the engine's fragment-packed layout (zk_pack_weights; rows padded to 64). */
 int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
                  float* Cpart, void* Cout, const int32_t* skip, void* stream);
-/* The split-K projection + residual add of a decode block in ONE launch (16 < M <= 128; replaces
- * zk_gemm_bf16(mode 0) + zk_resid_ln for the out_proj / fc2 of _torch.py:100-101): the column tile's
- * last-arriving workgroup sums the nsplit fp32 slabs in split order (part: [nsplit][M][N], written
- * write-through), updates x[M][N] = bf16(x + bf16(sum)) in place and writes stats[M][T][2] = (mean, M2)
- * of its x columns (T = zk_gemm_resid_tiles) for the next GEMM's LayerNorm (zk_gemm_ln). cnt: T int32
- * tile counters, zero before the first call (each call leaves them zero). */
-int zk_gemm_resid(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, float* part,
-                  void* x, float* stats, int* cnt, const int32_t* skip, void* stream);
-/* The GEMM after a zk_gemm_resid: C = LayerNorm(x) . W^T with the LayerNorm (weight / bias, eps) applied
- * while the activation x (the residual stream, bf16 [M][lda]) is staged, from the T per-tile row
- * statistics zk_gemm_resid wrote (Chan's combination: equal to the two-pass LayerNorm of k_resid_ln up
- * to fp32 rounding). mode 0 / 1 as zk_gemm_bf16; 16 < M <= 128; the decode block's in_proj, fc1 and
- * heads shapes. Together they replace zk_resid_ln between two GEMMs (_torch.py:100-101). */
-int zk_gemm_ln(const void* x, long lda, const void* W, int M, int N, int K, int nsplit, int mode, float* Cpart,
-               void* Cout, const void* ln_w, const void* ln_b, float eps, const float* stats, int T,
-               const int32_t* skip, void* stream);
-/* Host-only: T, the column tiles (statistics per row) of zk_gemm_resid at this shape; 0 = unsupported. */
-int zk_gemm_resid_tiles(int M, int N, int K, int nsplit);
-/* Host-only: 1 when zk_gemm_ln takes this shape (mode, T statistics per row). */
-int zk_gemm_ln_supported(int M, int N, int K, int nsplit, int mode, int T);
 /* Host-only (no GPU): the number of 16-column tiles of W's packed image that the L2 warm-up of
  * this decode GEMM (warm.h: issued by the kernel before it) reads; 0 when the GEMM is not warmed.
  * Never more than ceil(N / 16), the tiles of the packed image that hold a column < N. */
@@ -292,16 +272,6 @@ typedef struct zk_step_desc {
     float* dbg;                    /* nullable: fp32 CFG logits of draw 0 */
     zk_gen_state st;
     zk_sampling_params sp;
-    /* fuse_resid = 1 (16 < 2B <= 128, zk_gemm_ln_supported shapes): each block's out_proj and fc2 run as
-     * zk_gemm_resid (split-K reduce + residual add in their own tail) and the following in_proj / fc1 /
-     * heads as zk_gemm_ln (LayerNorm applied while staging), without zk_resid_ln launches. Buffers:
-     * row statistics fp32 [2B][T][2] after out_proj (stats_o) and after fc2 (stats_f), tile counters
-     * int32 [T] (zero before the first step; every step leaves them zero). 0: the launch sequence above. */
-    int32_t fuse_resid, pad_[3];
-    float* stats_o;
-    float* stats_f;
-    int32_t* cnt_o;
-    int32_t* cnt_f;
 } zk_step_desc;
 
 int zk_decode_step(const zk_step_desc* d, void* stream);

@@ -154,102 +154,6 @@ def test_prefill_gemm_epilogues_consistent(M, N, K):
     assert float((d > 0).float().mean()) < 1e-3
 
 
-@pytest.mark.parametrize("M,N,K,nsplit", [(128, 2048, 2048, 4), (128, 2048, 8192, 8), (100, 2048, 4096, 4),
-                                          (24, 1024, 2048, 2)])
-def test_gemm_resid_equals_gemm_plus_resid_ln(M, N, K, nsplit):
-    """zk_gemm_resid (split-K GEMM whose per-tile last arriver reduces the slabs and adds the residual,
-    round 5) == zk_gemm_bf16 + zk_resid_ln's residual output, bit for bit; the per-tile row statistics
-    are the mean / M2 of the bf16 x over each tile's columns; the counters are left at zero (a second
-    call gives the same x from the same input)."""
-    from zonos_amd import _lib
-    from zonos_amd._lib import call, ptr, stream_ptr
-    from zonos_amd.engine import pack_weights
-    s = stream_ptr()
-    g = torch.Generator(device="cpu").manual_seed(M + K)
-    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
-    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
-    x0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(DEV)
-    Wpk = pack_weights(W, s)
-    part = torch.empty(nsplit * M * N, device=DEV)
-    xr, xn = x0.clone(), torch.empty_like(x0)
-    w = torch.ones(N, dtype=torch.bfloat16, device=DEV)
-    b = torch.zeros(N, dtype=torch.bfloat16, device=DEV)
-    call("zk_gemm_bf16", ptr(A), K, ptr(Wpk), M, N, K, nsplit, 0, ptr(part), None, None, s)
-    call("zk_resid_ln", ptr(part), nsplit, ptr(xr), ptr(w), ptr(b), 1e-5, M, N, ptr(xr), ptr(xn), 0, None, s)
-    T = _lib.load().zk_gemm_resid_tiles(M, N, K, nsplit)
-    assert T > 0 and N % T == 0
-    stats = torch.full((M, T, 2), float("nan"), device=DEV)
-    cnt = torch.zeros(T, dtype=torch.int32, device=DEV)
-    for rep in range(2):
-        x = x0.clone()
-        call("zk_gemm_resid", ptr(A), K, ptr(Wpk), M, N, K, nsplit, ptr(part), ptr(x), ptr(stats), ptr(cnt), None, s)
-        torch.cuda.synchronize()
-        assert torch.equal(x, xr), (rep, (x.float() - xr.float()).abs().max())
-        assert int(cnt.abs().sum()) == 0
-    xt = x.float().view(M, T, N // T)
-    mean = xt.mean(-1)
-    m2 = ((xt - mean[..., None]) ** 2).sum(-1)
-    assert torch.allclose(stats[..., 0], mean, rtol=1e-5, atol=1e-6), (stats[..., 0] - mean).abs().max()
-    assert torch.allclose(stats[..., 1], m2, rtol=1e-4, atol=1e-5), (stats[..., 1] - m2).abs().max()
-
-
-@pytest.mark.parametrize("M,N,K,nsplit,mode,Kp,Np,psplit", [
-    (128, 3072, 2048, 4, 0, 8192, 2048, 8),      # in_proj after fc2 (T = 32)
-    (128, 16384, 2048, 1, 1, 2048, 2048, 4),     # fc1 (SwiGLU) after out_proj (T = 64: 32-column tiles)
-    (128, 9234, 2048, 1, 0, 8192, 2048, 8),      # heads after the last fc2 (narrow 48-column workgroups)
-    (40, 16384, 2048, 1, 1, 2048, 2048, 4)])     # fc1 at B = 20 (T = 32: 64-column tiles at M <= 64)
-def test_gemm_ln_equals_resid_ln_then_gemm(M, N, K, nsplit, mode, Kp, Np, psplit):
-    """zk_gemm_resid + zk_gemm_ln (LayerNorm applied while staging, from the producer's per-tile row
-    statistics) against the launch pair zk_gemm_bf16 + zk_resid_ln + zk_gemm_bf16 on xn: the LayerNorm
-    statistics differ only in fp32 rounding (Chan's combination vs two passes), so the outputs agree to
-    a bf16 ulp of a few activations."""
-    from zonos_amd import _lib
-    from zonos_amd._lib import call, ptr, stream_ptr
-    from zonos_amd.engine import pack_weights
-    s = stream_ptr()
-    g = torch.Generator(device="cpu").manual_seed(N + M)
-    D = K
-    Ap = torch.randn(M, Kp, generator=g).to(torch.bfloat16).to(DEV)
-    Wp = pack_weights((torch.randn(Np, Kp, generator=g) / Kp ** 0.5).to(torch.bfloat16).to(DEV), s)
-    x0 = (2 * torch.randn(M, D, generator=g) + 0.3).to(torch.bfloat16).to(DEV)
-    lw = (1 + 0.1 * torch.randn(D, generator=g)).to(torch.bfloat16).to(DEV)
-    lb = (0.1 * torch.randn(D, generator=g)).to(torch.bfloat16).to(DEV)
-    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
-    if mode == 1:
-        Wperm = torch.empty_like(W)
-        call("zk_permute_fc1", ptr(W), N // 2, K, ptr(Wperm), s)
-        W = Wperm
-    Wpk = pack_weights(W, s)
-    part = torch.empty(max(psplit * M * Np, nsplit * M * N), device=DEV)
-    # reference: slabs -> resid_ln -> xn -> GEMM
-    x1, xn = x0.clone(), torch.empty_like(x0)
-    call("zk_gemm_bf16", ptr(Ap), Kp, ptr(Wp), M, Np, Kp, psplit, 0, ptr(part), None, None, s)
-    call("zk_resid_ln", ptr(part), psplit, ptr(x1), ptr(lw), ptr(lb), 1e-5, M, D, ptr(x1), ptr(xn), 0, None, s)
-    out_ref = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV) if mode == 1 else None
-    C_ref = torch.empty(nsplit * M * N, device=DEV)
-    call("zk_gemm_bf16", ptr(xn), D, ptr(Wpk), M, N, K, nsplit, mode, ptr(C_ref), ptr(out_ref), None, s)
-    # fused: zk_gemm_resid -> zk_gemm_ln
-    T = _lib.load().zk_gemm_resid_tiles(M, Np, Kp, psplit)
-    assert _lib.load().zk_gemm_ln_supported(M, N, K, nsplit, mode, T)
-    x2 = x0.clone()
-    stats = torch.empty(M * T * 2, device=DEV)
-    cnt = torch.zeros(T, dtype=torch.int32, device=DEV)
-    call("zk_gemm_resid", ptr(Ap), Kp, ptr(Wp), M, Np, Kp, psplit, ptr(part), ptr(x2), ptr(stats), ptr(cnt), None, s)
-    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV) if mode == 1 else None
-    C = torch.empty(nsplit * M * N, device=DEV)
-    call("zk_gemm_ln", ptr(x2), D, ptr(Wpk), M, N, K, nsplit, mode, ptr(C), ptr(out), ptr(lw), ptr(lb), 1e-5,
-         ptr(stats), T, None, s)
-    torch.cuda.synchronize()
-    assert torch.equal(x1, x2)
-    if mode == 1:
-        got, ref = out.float(), out_ref.float()
-    else:
-        got, ref = C.view(nsplit, M, N).sum(0), C_ref.view(nsplit, M, N).sum(0)
-    d = (got - ref).abs()
-    scale = ref.abs().mean()
-    assert d.max() <= 0.02 * scale + 1e-3 and d.mean() <= 1e-3 * scale, (float(d.max()), float(d.mean()), float(scale))
-
-
 def test_pack_weights_layout():
     """Fragment-packed layout: block (nt, kc) lane l holds W[16nt + l%16][32kc + 8(l//16) .. +8]."""
     from zonos_amd._lib import stream_ptr

@@ -62,48 +62,6 @@ def gemm():
         del Ws
 
 
-def resid():
-    """Round 5: the block's out_proj / fc2 + residual add as zk_gemm_bf16 (mode 0) + zk_resid_ln (the shipped
-    pair) vs zk_gemm_resid (one launch, the column tile's last arriver reduces; no LayerNorm: that moves
-    to the next GEMM). Weights rotate over enough copies to stream from HBM; each pair is timed back to
-    back, as the decode step runs them."""
-    M = 128
-    for name, N, K, tgt in (("out_proj", 2048, 2048, 128), ("fc2", 2048, 8192, 256)):
-        ns = _split_for(N, K, M, tgt)
-        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
-        Ws = [torch.randn((N + 63) // 64 * 64, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
-        A = torch.randn(M, K, device=dev).to(torch.bfloat16)
-        part = torch.empty(ns * M * N, device=dev)
-        x = torch.randn(M, N, device=dev).to(torch.bfloat16)
-        xn = torch.empty_like(x)
-        w, b = torch.ones(N, device=dev).to(torch.bfloat16), torch.zeros(N, device=dev).to(torch.bfloat16)
-        T = _lib.load().zk_gemm_resid_tiles(M, N, K, ns)
-        stats = torch.empty(M * max(T, 1) * 2, device=dev)
-        cnt = torch.zeros(max(T, 1), dtype=torch.int32, device=dev)
-        it = [0]
-
-        def pair():
-            W = Ws[it[0] % ncopy]
-            it[0] += 1
-            call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, ns, 0, ptr(part), None, None, S)
-            call("zk_resid_ln", ptr(part), ns, ptr(x), ptr(w), ptr(b), 1e-5, M, N, ptr(x), ptr(xn), 0, None, S)
-
-        def gemm_only():
-            W = Ws[it[0] % ncopy]
-            it[0] += 1
-            call("zk_gemm_bf16", ptr(A), K, ptr(W), M, N, K, ns, 0, ptr(part), None, None, S)
-
-        def fused():
-            W = Ws[it[0] % ncopy]
-            it[0] += 1
-            call("zk_gemm_resid", ptr(A), K, ptr(W), M, N, K, ns, ptr(part), ptr(x), ptr(stats), ptr(cnt), None, S)
-        for label, fn in (("gemm + resid_ln", pair), ("gemm alone", gemm_only), ("gemm_resid", fused)):
-            x.normal_()
-            us = timeit(fn)
-            print(f"resid {name:8s} split={ns} T={T}: {label:16s} {us:7.2f} us", flush=True)
-        del Ws
-
-
 def sweep():
     """Fixed cost vs streamed bytes of the decode GEMM family: k_gemm_ws (M = 128, split 4) and the
     B <= 8 GEMV (M = 2, split 1) at N = 2048 / 8192 over K = 512 .. 8192; fit t = t0 + bytes / rate."""
@@ -421,8 +379,6 @@ if __name__ == "__main__":
         gemm()
     if what == "sweep":
         sweep()
-    if what == "resid":
-        resid()
     if what in ("mamba",):
         mamba()
     if what in ("attn_small",):

@@ -46,8 +46,7 @@ class StepDesc(C.Structure):
                                          "attn_merge", "rope_neox", "small")] + \
               [("eps", F), ("layers", P), ("emb", P), ("heads", P), ("lnf_w", P), ("lnf_b", P), ("freqs", P),
                ("x", P), ("xn", P), ("y", P), ("h", P), ("part", P), ("attn_work", P), ("attn_cnt", P), ("dbg", P),
-               ("st", GenState), ("sp", SamplingParams), ("fuse_resid", C.c_int32), ("pad_", C.c_int32 * 3),
-               ("stats_o", P), ("stats_f", P), ("cnt_o", P), ("cnt_f", P)]
+               ("st", GenState), ("sp", SamplingParams)]
 
 
 class HybridLayer(C.Structure):
@@ -97,8 +96,6 @@ _SIGS = {
     "zk_resid_ln": [P, I, P, P, P, F, I, I, P, P, I, P, P],
     "zk_gemm_bf16": [P, L, P, I, I, I, I, I, P, P, P, P],
     "zk_gemv_fused": [P, L, P, I, I, I, I, P, P, F, P, P, P, P],
-    "zk_gemm_resid": [P, L, P, I, I, I, I, P, P, P, P, P, P],
-    "zk_gemm_ln": [P, L, P, I, I, I, I, I, P, P, P, P, F, P, I, P, P],
     "zk_permute_fc1": [P, I, I, P, P],
     "zk_pack_weights": [P, I, I, P, P],
     "zk_qkv_rope": [P, I, I, I, I, I, I, P, I, P, P, P, P, I, P, I, P, P],
@@ -177,18 +174,13 @@ def load():
     lib.zk_dac_resunit_supported.argtypes = [I]
     lib.zk_gemm_warm_tiles.restype = C.c_int
     lib.zk_gemm_warm_tiles.argtypes = [I, I, I, I, I, I]
-    lib.zk_gemm_resid_tiles.restype = C.c_int
-    lib.zk_gemm_resid_tiles.argtypes = [I, I, I, I]
-    lib.zk_gemm_ln_supported.restype = C.c_int
-    lib.zk_gemm_ln_supported.argtypes = [I, I, I, I, I, I]
     _lib = lib
     return lib
 
 
 def exported_symbols() -> list[str]:
     return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_abi_size",
-                          "zk_dac_decode_workspace", "zk_dac_resunit_supported", "zk_gemm_warm_tiles",
-                          "zk_gemm_resid_tiles", "zk_gemm_ln_supported"]
+                          "zk_dac_decode_workspace", "zk_dac_resunit_supported", "zk_gemm_warm_tiles"]
 
 
 def call(name: str, *args):

@@ -39,7 +39,6 @@ extern "C" long zk_abi_size(int which) {
         case 13: return (long)offsetof(zk_step_desc, eps);
         case 14: return (long)offsetof(zk_step_desc, st);
         case 15: return (long)offsetof(zk_step_desc, sp);
-        case 22: return (long)offsetof(zk_step_desc, stats_o);
         case 8: return (long)sizeof(zk_dac_desc);
         case 16: return (long)offsetof(zk_dac_desc, blocks);
         case 17: return (long)sizeof(zk_dac_block);
@@ -171,27 +170,6 @@ extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
                                   stream));
             ZK_STEP(zk_gemv_fused(d->h, Fd, L.fc2, R, D, Fd, 2, nullptr, nullptr, d->eps, nullptr, d->x, skip,
                                   stream));
-        } else if (d->fuse_resid) {
-            // no k_resid_ln: out_proj / fc2 reduce their split-K slabs and add the residual in their own
-            // tail (zk_gemm_resid), in_proj / fc1 / heads apply the LayerNorm while staging (zk_gemm_ln)
-            const int To = zk_gemm_resid_tiles(R, D, H * hd, d->split_o), Tf = zk_gemm_resid_tiles(R, D, Fd, d->split_fc2);
-            if (i == 0)
-                ZK_STEP(zk_gemm_bf16(d->xn, D, L.wqkv, R, Nqkv, D, d->split_qkv, 0, d->part, nullptr, skip, stream));
-            else
-                ZK_STEP(zk_gemm_ln_warm(d->x, D, L.wqkv, R, Nqkv, D, d->split_qkv, 0, d->part, nullptr, L.ln1_w, L.ln1_b,
-                                        d->eps, d->stats_f, Tf, skip, ZkWarm{nullptr, 0, 0, 0, 0}, stream));
-            ZK_STEP(zk_attn_decode_qkv_sc(d->part, d->split_qkv, d->freqs, L.k_cache, L.vt_cache, R, H, Hk, hd,
-                                          d->smax, 1, pos, d->attn_work, d->attn_splits, d->attn_cnt, d->y,
-                                          d->rope_neox, skip, stream));
-            ZK_STEP(zk_gemm_resid_warm(d->y, H * hd, L.wo, R, D, H * hd, d->split_o, d->part, d->x, d->stats_o, d->cnt_o,
-                                       skip, warm_desc(L.fc1, R, 2 * Fd, D, 1, 1), stream));
-            ZK_STEP(zk_gemm_ln_warm(d->x, D, L.fc1, R, 2 * Fd, D, 1, 1, nullptr, d->h, L.ln2_w, L.ln2_b, d->eps,
-                                    d->stats_o, To, skip, warm_desc(L.fc2, R, D, Fd, d->split_fc2), stream));
-            const bool last = i + 1 == d->n_layer;
-            const ZkWarm next = last ? warm_desc(d->heads, R, K * V, D, d->split_heads)
-                                     : warm_desc(d->layers[i + 1].wqkv, R, Nqkv, D, d->split_qkv);
-            ZK_STEP(zk_gemm_resid_warm(d->h, Fd, L.fc2, R, D, Fd, d->split_fc2, d->part, d->x, d->stats_f, d->cnt_f,
-                                       skip, next, stream));
         } else {
             ZK_STEP(zk_gemm_bf16(d->xn, D, L.wqkv, R, Nqkv, D, d->split_qkv, 0, d->part, nullptr, skip, stream));
             ZK_STEP(zk_attn_decode_qkv_sc(d->part, d->split_qkv, d->freqs, L.k_cache, L.vt_cache, R, H, Hk, hd,
@@ -216,10 +194,6 @@ extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
     if (d->small)
         ZK_STEP(zk_gemv_fused(d->x, D, d->heads, R, K * V, D, 0, d->lnf_w, d->lnf_b, d->eps, d->part, nullptr, skip,
                               stream));
-    else if (d->fuse_resid)
-        ZK_STEP(zk_gemm_ln_warm(d->x, D, d->heads, R, K * V, D, d->split_heads, 0, d->part, nullptr, d->lnf_w, d->lnf_b,
-                                d->eps, d->stats_f, zk_gemm_resid_tiles(R, D, Fd, d->split_fc2), skip,
-                                ZkWarm{nullptr, 0, 0, 0, 0}, stream));
     else
         ZK_STEP(zk_gemm_bf16(d->xn, D, d->heads, R, K * V, D, d->split_heads, 0, d->part, nullptr, skip, stream));
     const int nsp = d->small ? 1 : d->split_heads;

@@ -286,178 +286,13 @@ constexpr int ws_nld() {
     while (n > 1 && n < 2 * MT && (2 * MT) % n != 0) --n;
     return n;
 }
-// MODE 2 -- split-K reduction + residual add in the GEMM's own tail (the out_proj / fc2 of a decode
-// block, _torch.py:100-101), instead of a k_resid_ln launch. Every workgroup stores its fp32 slab tile
-// write-through (sc1), drains it (every storing wave: s_waitcnt vmcnt(0)), and one lane takes a ticket
-// on the column tile's counter (relaxed agent-scope add; MI355X_MICROARCH.md visibility table, first
-// row: the workgroup whose add returns nsplit - 1 is the last, and it reads the tile's slabs with sc1
-// loads only). No workgroup waits for another: the last arriver of a tile does the work, so there is
-// no spin. It sums the nsplit slabs in split order (the order of k_resid_ln: bit-identical sums),
-// forms x = bf16(x + bf16(sum)) over its columns in place, and writes per-row statistics of those
-// BNW columns (mean, M2 of the bf16 x) for the consumer's LayerNorm (k_gemm_ws LNA: Chan's combination
-// over the row's tiles), then resets the counter for the next launch.
-template <int BNW, int MT, int NCW>
-ZK_DEV void ws_tile_combine(const float* Cpart, int M, int N, int nsplit, int n0, int bx, int gx, int w, int lane,
-                            char* smem, int* tc_cnt, bf16_t* tc_x, float* tc_stats) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave: its sc1 stores drained
-    int* flag = reinterpret_cast<int*>(smem + WS_NB * (MT * 16 * BK * 2) - 16);
-    __syncthreads();
-    if (w == 0 && lane == 0) {
-        const int t = __hip_atomic_fetch_add(tc_cnt + bx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = (t == nsplit - 1);
-    }
-    __syncthreads();
-    if (!*flag) return;
-    if (w == 0 && lane == 0) __hip_atomic_store(tc_cnt + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    constexpr int LPR = BNW / 4, RPI = 64 / LPR, NQI = (MT * 16 + RPI - 1) / RPI;
-    const int c4 = (lane % LPR) * 4;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Cpart), (short)0,
-                                                                        0x7fffffff, 0x00020000);
-    const size_t slab = (size_t)M * N;
-#pragma unroll
-    for (int q = w; q < NQI; q += NCW) {
-        const int m = q * RPI + lane / LPR;
-        const bool ok = lane < RPI * LPR && m < M && n0 + c4 < N;
-        const int mm = ok ? m : 0, cc = ok ? n0 + c4 : 0;
-        f32x4 a[8];
-#pragma unroll
-        for (int sp = 0; sp < 8; ++sp)
-            if (sp < nsplit)
-                a[sp] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rs, (int)(((size_t)sp * slab + (size_t)mm * N + cc) * 4), 0, 16));
-        const uint2 xo = *reinterpret_cast<const uint2*>(tc_x + (size_t)mm * N + cc);
-        f32x4 acc = a[0];
-#pragma unroll
-        for (int sp = 1; sp < 8; ++sp)
-            if (sp < nsplit) acc = acc + a[sp];
-        float xi[4] = {__uint_as_float(xo.x << 16), __uint_as_float(xo.x & 0xffff0000u), __uint_as_float(xo.y << 16),
-                       __uint_as_float(xo.y & 0xffff0000u)};
-        float xv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] = round_bf(xi[e] + round_bf(acc[e]));     // x = bf16(x + bf16(proj))
-        if (ok) *reinterpret_cast<uint2*>(tc_x + (size_t)m * N + cc) = make_uint2(pack2(xv[0], xv[1]), pack2(xv[2], xv[3]));
-        // row statistics of this tile's BNW columns: the row's LPR lanes are consecutive (LPR | 64)
-        float sm = ok ? (xv[0] + xv[1]) + (xv[2] + xv[3]) : 0.f;
-#pragma unroll
-        for (int o = LPR / 2; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
-        const float mean = sm / (float)BNW;
-        float m2 = 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { const float d = xv[e] - mean; m2 += d * d; }
-        if (!ok) m2 = 0.f;
-#pragma unroll
-        for (int o = LPR / 2; o > 0; o >>= 1) m2 += __shfl_xor(m2, o, 64);
-        if (ok && lane % LPR == 0)
-            *reinterpret_cast<float2*>(tc_stats + ((size_t)m * gx + bx) * 2) = make_float2(mean, m2);
-    }
-}
-
-// LNA -- the activation is the residual stream x (bf16 [M][lda]) of the previous block and the
-// LayerNorm in front of this GEMM (_torch.py:100-101 norm / norm2, :80 norm_f) is applied by the
-// loader waves while they stage it, from the per-tile row statistics the producing zk_gemm_resid left
-// (ws_tile_combine): no k_resid_ln launch and no xn round trip. The loaders then load to registers,
-// normalise and write the same lane-linear LDS image the LDS-DMA form writes, so the compute waves
-// are unchanged. Row statistics: the LT tile (mean, M2) pairs of a row combined in a fixed xor tree
-// (Chan, Golub & LeVeque), var = M2 / K, then nn.LayerNorm's y = ((x * rstd) + (-rstd * mean)) * w + b.
-struct ZkLna {
-    const bf16_t* w;        // LayerNorm weight / bias (bf16 [K])
-    const bf16_t* b;
-    const float* stats;     // [M][LT][2] (mean, M2) per producer column tile
-    float eps;
-};
-
-template <int MT, int NLD, int NCH, int LT>
-ZK_DEV void ws_loader_lna(const bf16_t* __restrict__ A, long lda, int M, int K, int kbeg, int ld, int lane, char* smem,
-                          const ZkLna& lna) {
-    constexpr int NP = 2 * MT / NLD;                   // pieces (8 rows x 128 B) per loader per chunk
-    static_assert((2 * MT) % NLD == 0 && LT >= 8 && LT <= 64 && (LT & (LT - 1)) == 0, "LNA loader shape");
-    constexpr int RS = WS_DA + 1;                      // register slots (chunks in flight + the one staged)
-    const int rl = lane >> 3, sl = lane & 7;
-    const int cofs = (sl ^ rl) << 3;                   // this lane's 8 columns of every 64-column chunk
-    // ---- statistics of this wave's 8 NP rows (row q = 8 j + r of the wave: tile row 8 (j NLD + ld) + r),
-    // RPT rows per pass, lane (g, t) holding tile t of the pass's row g
-    constexpr int RPT = 64 / LT, NPASS = 8 * NP / RPT;
-    float2 st[NPASS];
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-        const int q = p * RPT + lane / LT;
-        const int row = 8 * ((q >> 3) * NLD + ld) + (q & 7);
-        st[p] = *reinterpret_cast<const float2*>(lna.stats + ((size_t)min(row, M - 1) * LT + (lane % LT)) * 2);
-    }
-    // the first chunks' rows and LayerNorm columns, issued before the statistics are waited for
-    uint4 xr[RS][NP], wr[RS], br[RS];
-    auto issue = [&](int ch, int slot) {
-        const int k0 = kbeg + ch * BK;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            const int row = 8 * (j * NLD + ld) + rl;
-            xr[slot][j] = *reinterpret_cast<const uint4*>(A + (size_t)min(row, M - 1) * lda + k0 + cofs);
-        }
-        wr[slot] = *reinterpret_cast<const uint4*>(lna.w + k0 + cofs);
-        br[slot] = *reinterpret_cast<const uint4*>(lna.b + k0 + cofs);
-    };
-#pragma unroll
-    for (int c = 0; c < WS_DA && c < NCH; ++c) issue(c, c % RS);
-    float rstd[NP], nb[NP];
-    const float c0 = (float)(K / LT);                  // elements per producer tile
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-        float mean = st[p].x, m2 = st[p].y, cnt = c0;
-#pragma unroll
-        for (int o = 1; o < LT; o <<= 1) {             // Chan: two halves of cnt elements each
-            const float mo = __shfl_xor(mean, o, 64), m2o = __shfl_xor(m2, o, 64);
-            const float d = mo - mean;
-            m2 = (m2 + m2o) + d * d * (cnt * 0.5f);
-            mean = (mean + mo) * 0.5f;
-            cnt *= 2.f;
-        }
-        const float rs = 1.0f / sqrtf(m2 / (float)K + lna.eps);
-        const float nbv = -rs * mean;
-#pragma unroll
-        for (int g = 0; g < RPT; ++g) {
-            const int q = p * RPT + g;                 // compile-time: row q = 8 j + r of the wave
-            const float a = __shfl(rs, g * LT, 64), bb = __shfl(nbv, g * LT, 64);
-            if (rl == (q & 7)) {
-                rstd[q >> 3] = a;
-                nb[q >> 3] = bb;
-            }
-        }
-    }
-    auto stage = [&](int ch, int slot) {
-        char* dst = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
-        float wf[8], bf[8];
-        unpack8(wr[slot], wf);
-        unpack8(br[slot], bf);
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            float xf[8], o[8];
-            unpack8(xr[slot][j], xf);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(xf[e], rstd[j]), nb[j]), wf[e]), bf[e]);
-            *reinterpret_cast<uint4*>(dst + (j * NLD + ld) * 1024 + lane * 16) = pack8(o);
-        }
-    };
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        // barrier c publishes chunk c + 1 (and, the first, chunk 0), as the LDS-DMA loaders do
-        if (c == 0) stage(0, 0);
-        if (c + 1 < NCH) stage(c + 1, (c + 1) % RS);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (c + WS_DA < NCH) issue(c + WS_DA, (c + WS_DA) % RS);
-    }
-}
-
-template <int MODE, int NCH, int PF, int MT, int NCW = 4, int NG = 1, int NB = (NCW > 5 ? 1 : 2), int LT = 0>
+template <int MODE, int NCH, int PF, int MT, int NCW = 4, int NG = 1, int NB = (NCW > 5 ? 1 : 2)>
 __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_gemm_ws(const bf16_t* __restrict__ A, long lda,
                                                            const bf16_t* __restrict__ W, int M, int N, int K,
                                                            int kslice, float* __restrict__ Cpart,
                                                            bf16_t* __restrict__ Cout, const int32_t* skip,
                                                            const bf16_t* __restrict__ wW, int wK, int wgx, int wgz,
-                                                           int wch, int* __restrict__ tc_cnt, bf16_t* __restrict__ tc_x,
-                                                           float* __restrict__ tc_stats, ZkLna lna) {
+                                                           int wch) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // (the skip word is tested first here: deferring the test behind the first loads, as k_gemv_f
     // does, measured 0.3-1.2 % slower per c3 step with a vector or a scalar load of the word,
@@ -475,9 +310,6 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
     constexpr int NLD = ws_nld<NCW, MT>();
     static_assert(NLD >= 1 && (NLD >= 2 * MT || (2 * MT) % NLD == 0),
                   "every loader wave must issue the same number of pieces per chunk (its vmcnt waits count NP)");
-    static_assert(MODE != 2 || (ZK_WS_EPI && NG == 1 && (BNW == 32 || BNW == 64)),
-                  "tile combine: staged epilogue, 32- or 64-column workgroups (power-of-two lanes per row)");
-    static_assert(LT == 0 || (MT == 8 && NG == 1), "LNA: the 128-row form");
     if (w >= NCW) {
         // ---------------- loader wave(s): 2*MT x 1 KB LDS-DMA pieces per chunk (16*MT rows x 64 k),
         // loader l moving pieces l, l + NLD, ...
@@ -486,9 +318,6 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
         constexpr int NP = (2 * MT + NLD - 1) / NLD;      // pieces per loader per chunk
         const int ld = __builtin_amdgcn_readfirstlane(w - NCW);   // wave-uniform: scalar piece loop
         const int rl = lane >> 3, sl = lane & 7;
-        if constexpr (LT > 0) {
-            ws_loader_lna<MT, NLD, NCH, LT>(A, lda, M, K, kbeg, ld, lane, smem, lna);
-        } else {
         auto issue = [&](int ch) {
             char* dst = smem + (ch % WS_NB) * (MT * 16 * BK * 2);
             const int k0 = kbeg + ch * BK;
@@ -522,7 +351,6 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
             __builtin_amdgcn_s_barrier();                           // publish chunk `need`
             asm volatile("" ::: "memory");
             if (c + WS_DA < nchunks) issue(c + WS_DA);              // its slot was read >= 2 chunks ago
-        }
         }
         if (wW != nullptr) {
             // L2 warm-up of the NEXT GEMM (warm.h): its workgroups L, L + nwg, ... run on this XCD;
@@ -634,9 +462,9 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
                     // 16-column group); SwiGLU runs in the store pass below, on every lane (here it
                     // would run on half the lanes behind a branch per value: fc1 23.4 -> 18.x us)
                     tile[(mt * 16 + lg * 4 + i) * TS + (w * NG + g) * 16 + ln] =
-                        MODE != 1 ? acc[g][mt][i] : round_bf(acc[g][mt][i]);
+                        MODE == 0 ? acc[g][mt][i] : round_bf(acc[g][mt][i]);
         __syncthreads();
-        if (MODE == 0 || MODE == 2) {
+        if (MODE == 0) {
             float* C = Cpart + (size_t)split * M * N;
             constexpr int LPR = BNW / 4;                         // lanes per row (4 floats each)
             constexpr int RPI = 64 / LPR;                        // whole rows per instruction
@@ -649,7 +477,7 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
                     const f32x4 v = *reinterpret_cast<const f32x4*>(tile + m * TS + c4);
                     float* dst = C + (size_t)m * N + n0 + c4;
                     if (n0 + c4 + 3 < N) {
-                        if constexpr (ZK_SLAB_SC1 || MODE == 2)      // (MODE 2: write-through, see tile_combine)
+                        if constexpr (ZK_SLAB_SC1)
                             asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
                         else if constexpr (ZK_SLAB_NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
                         else *reinterpret_cast<f32x4*>(dst) = v;
@@ -658,9 +486,6 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
                     }
                 }
             }
-            if constexpr (MODE == 2)
-                ws_tile_combine<BNW, MT, NCW>(Cpart, M, N, gridDim.z, n0, bx, gridDim.x, w, lane, smem, tc_cnt, tc_x,
-                                              tc_stats);
         } else {
             const int F = N / 2;
             constexpr int GPR = BNW / 16;                        // 16-column groups per row
@@ -1247,106 +1072,18 @@ extern "C" int zk_gemm_warm_tiles(int M, int N, int K, int nsplit, int mode, int
 
 extern "C" int zk_gemm_bf16(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
                             float* Cpart, void* Cout, const int32_t* skip_flag, void* stream) {
-    ZK_REQUIRE(mode == 0 || mode == 1, "zk_gemm_bf16: mode %d (0 or 1)", mode);
     return zk_gemm_bf16_warm(A, lda, W, M, N, K, nsplit, mode, Cpart, Cout, skip_flag, ZkWarm{nullptr, 0, 0, 0, 0},
                              stream);
 }
 
-// zk_gemm_resid (include/zonos_hip.h): the split-K projection + residual add of a decode block in one
-// launch (MODE 2, ws_tile_combine), 16 < M <= 128.
-extern "C" int zk_gemm_resid(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, float* part,
-                             void* x, float* stats, int* cnt, const int32_t* skip_flag, void* stream) {
-    return zk_gemm_bf16_warm(A, lda, W, M, N, K, nsplit, 2, part, nullptr, skip_flag, ZkWarm{nullptr, 0, 0, 0, 0},
-                             stream, cnt, x, stats);
-}
-int zk_gemm_resid_warm(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, float* part, void* x,
-                       float* stats, int* cnt, const int32_t* skip_flag, ZkWarm warm, void* stream) {
-    return zk_gemm_bf16_warm(A, lda, W, M, N, K, nsplit, 2, part, nullptr, skip_flag, warm, stream, cnt, x, stats);
-}
-
-// zk_gemm_ln (include/zonos_hip.h): the GEMM after a zk_gemm_resid, its LayerNorm applied while the
-// activation is staged (k_gemm_ws LNA). The 128-row form; the instantiations the decode block uses:
-// in_proj (split 4: 8 chunks), fc1 (SwiGLU: 32) and the heads (32), after producers of 32- or
-// 64-column tiles (LT = 64 or 32 statistics per row).
-int zk_gemm_ln_warm(const void* x, long lda, const void* W, int M, int N, int K, int nsplit, int mode, float* Cpart,
-                    void* Cout, const void* ln_w, const void* ln_b, float eps, const float* stats, int T,
-                    const int32_t* skip_flag, ZkWarm warm, void* stream) {
-    ZK_REQUIRE(M > 16 && M <= BM && N > 0 && K > 0 && nsplit >= 1 && K % (nsplit * BK) == 0,
-               "zk_gemm_ln: M=%d N=%d K=%d nsplit=%d (16 < M <= 128)", M, N, K, nsplit);
-    ZK_REQUIRE(mode == 0 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_ln: bad mode/nsplit");
-    ZK_REQUIRE(lda >= K && lda % 8 == 0 && ln_w && ln_b && stats && (T == 32 || T == 64) && K % T == 0,
-               "zk_gemm_ln: lda=%ld T=%d", lda, T);
-    const int nchunks = K / nsplit / BK;
-    const int ng = ws_ng(N, mode);
-    const int ncw = ws_ncw(M, N, nsplit, mode, ng);
-    ZK_REQUIRE(ng == 1 && (ncw == 3 || ncw == 4), "zk_gemm_ln: workgroup form ncw=%d ng=%d", ncw, ng);
-    const size_t lds = (size_t)WS_NB * 8 * 16 * BK * 2 + (warm.W ? 1024 : 0);
-    dim3 g((N + 16 * ncw - 1) / (16 * ncw), 1, nsplit);
-    const ZkLna lna{(const bf16_t*)ln_w, (const bf16_t*)ln_b, stats, eps};
-    bool handled = false;
-#define ZK_LN_LAUNCH(MODE_, NCH_, NCW_, LT_)                                                                        \
-    do {                                                                                                          \
-        auto kern_ = &k_gemm_ws<MODE_, NCH_, (MODE_ == 1 ? WS_PF : WS_PF0), 8, NCW_, 1, 2, LT_>;                  \
-        if (lds > 65536)                                                                                          \
-            hipFuncSetAttribute(reinterpret_cast<const void*>(kern_), hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                (int)lds);                                                                        \
-        hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW_ + ws_nld<NCW_, 8>())), lds, (hipStream_t)stream,            \
-                           (const bf16_t*)x, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
-                           skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks, nullptr,      \
-                           nullptr, nullptr, lna);                                                                \
-        handled = true;                                                                                           \
-    } while (0)
-#define ZK_LN_T(MODE_, NCH_, NCW_)                                   \
-    do {                                                              \
-        if (T == 32) ZK_LN_LAUNCH(MODE_, NCH_, NCW_, 32);             \
-        else ZK_LN_LAUNCH(MODE_, NCH_, NCW_, 64);                     \
-    } while (0)
-    if (mode == 1 && nchunks == 32 && ncw == 4) ZK_LN_T(1, 32, 4);
-    else if (mode == 0 && nchunks == 8 && ncw == 4) ZK_LN_T(0, 8, 4);
-    else if (mode == 0 && nchunks == 32 && ncw == 4) ZK_LN_T(0, 32, 4);
-    else if (mode == 0 && nchunks == 32 && ncw == 3) ZK_LN_T(0, 32, 3);
-#undef ZK_LN_T
-#undef ZK_LN_LAUNCH
-    ZK_REQUIRE(handled, "zk_gemm_ln: no instantiation for mode %d, %d chunks, %d waves", mode, nchunks, ncw);
-    ZK_CHECK_LAUNCH("zk_gemm_ln");
-    return 0;
-}
-
-// host mirror of zk_gemm_ln's instantiation choice: 1 when it takes this shape
-extern "C" int zk_gemm_ln_supported(int M, int N, int K, int nsplit, int mode, int T) {
-    if (M <= 16 || M > BM || nsplit < 1 || K % (nsplit * BK) != 0 || (T != 32 && T != 64) || K % T != 0) return 0;
-    if (mode == 1 && (nsplit != 1 || N % 16 != 0)) return 0;
-    const int nchunks = K / nsplit / BK, ng = ws_ng(N, mode), ncw = ws_ncw(M, N, nsplit, mode, ng);
-    if (ng != 1) return 0;
-    if (mode == 1) return nchunks == 32 && ncw == 4;
-    return mode == 0 && ((nchunks == 8 && ncw == 4) || (nchunks == 32 && (ncw == 4 || ncw == 3)));
-}
-
-extern "C" int zk_gemm_ln(const void* x, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
-                          float* Cpart, void* Cout, const void* ln_w, const void* ln_b, float eps, const float* stats,
-                          int T, const int32_t* skip_flag, void* stream) {
-    return zk_gemm_ln_warm(x, lda, W, M, N, K, nsplit, mode, Cpart, Cout, ln_w, ln_b, eps, stats, T, skip_flag,
-                           ZkWarm{nullptr, 0, 0, 0, 0}, stream);
-}
-
-// tiles per row of zk_gemm_resid's statistics (its workgroup columns), 0 if the shape is not supported
-extern "C" int zk_gemm_resid_tiles(int M, int N, int K, int nsplit) {
-    if (M <= 16 || M > BM || nsplit < 1 || K % (nsplit * BK) != 0 || K / nsplit / BK > 32) return 0;
-    const int ncw = ws_ncw(M, N, nsplit, 0, 1);
-    if ((ncw != 2 && ncw != 4) || N % (16 * ncw) != 0) return 0;
-    return N / (16 * ncw);
-}
-
 int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode,
-                      float* Cpart, void* Cout, const int32_t* skip_flag, ZkWarm warm, void* stream, int* tc_cnt,
-                      void* tc_x, float* tc_stats) {
+                      float* Cpart, void* Cout, const int32_t* skip_flag, ZkWarm warm, void* stream) {
     ZK_REQUIRE(M > 0 && N > 0 && K > 0, "zk_gemm_bf16: empty shape M=%d N=%d K=%d", M, N, K);
     ZK_REQUIRE(nsplit >= 1 && K % (nsplit * BK) == 0, "zk_gemm_bf16: K=%d must be a multiple of nsplit*%d", K, BK);
     ZK_REQUIRE(lda >= K && lda % 8 == 0, "zk_gemm_bf16: lda=%ld", lda);
-    ZK_REQUIRE(mode == 0 || mode == 2 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_bf16: bad mode/nsplit");
-    ZK_REQUIRE(mode != 2 || (M > 16 && M <= BM && K / nsplit / BK <= 32), "zk_gemm_resid: M=%d outside 17..128", M);
+    ZK_REQUIRE(mode == 0 || (mode == 1 && nsplit == 1 && N % 16 == 0), "zk_gemm_bf16: bad mode/nsplit");
     const int nchunks = K / nsplit / BK;
-    if (mode != 2 && M <= 16 && (K / nsplit) % 128 == 0) {
+    if (M <= 16 && (K / nsplit) % 128 == 0) {
         // weight-stream GEMV (B <= 8 decode): 2 column tiles per workgroup, K quarters per wave
         const int ks = K / nsplit / 128;
         dim3 g((N + 31) / 32, 1, nsplit);
@@ -1390,21 +1127,20 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
         // workgroups of 2 or 3 compute waves (16 columns each), the most that still fit one
         // workgroup per CU (the Mamba in_proj at 2 waves would be 266 workgroups for 256 CUs:
         // c5 decode 4.34 -> 4.64 ms); the same per-column K order (bit-identical results).
-        const int ncw = M > 16 ? ws_ncw(M, N, nsplit, mode == 2 ? 0 : mode, ng) : NCW;
+        const int ncw = M > 16 ? ws_ncw(M, N, nsplit, mode, ng) : NCW;
         dim3 g((N + 16 * ncw * ng - 1) / (16 * ncw * ng), 1, nsplit);
         const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 64 ? 4 : 8));
         const size_t lds = (size_t)WS_NB * MT * 16 * BK * 2 + (warm.W ? 1024 : 0);     // + warm-up sink
 #define ZK_WS_LAUNCH5(MODE_, NCH_, MT_, NG_, NCW_)                                                                 \
     do {                                                                                                          \
         constexpr int NB_ = NG_ > 1 ? ZK_WS_NGNB : (NCW_ > 5 ? 1 : 2);                                            \
-        auto kern_ = &k_gemm_ws<MODE_, NCH_, (MODE_ == 1 ? WS_PF : WS_PF0), MT_, NCW_, NG_, NB_>;                  \
+        auto kern_ = &k_gemm_ws<MODE_, NCH_, (MODE_ ? WS_PF : WS_PF0), MT_, NCW_, NG_, NB_>;                       \
         if (lds > 65536)                                                                                          \
             hipFuncSetAttribute(reinterpret_cast<const void*>(kern_), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 (int)lds);                                                                        \
         hipLaunchKernelGGL(kern_, g, dim3(64 * (NCW_ + ws_nld<NCW_, MT_>())), lds, (hipStream_t)stream,                \
                            (const bf16_t*)A, lda, (const bf16_t*)W, M, N, K, K / nsplit, Cpart, (bf16_t*)Cout,      \
-                           skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks, tc_cnt,       \
-                           (bf16_t*)tc_x, tc_stats, ZkLna{nullptr, nullptr, nullptr, 0.f});                       \
+                           skip_flag, (const bf16_t*)warm.W, warm.K, warm.gx, warm.gz, warm.chunks);              \
         handled = true;                                                                                           \
     } while (0)
 #define ZK_WS_LAUNCH4(MODE_, NCH_, MT_, NG_) ZK_WS_LAUNCH5(MODE_, NCH_, MT_, NG_, NCW)
@@ -1429,28 +1165,7 @@ int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int 
         }                                                                                                         \
     } while (0)
         bool handled = false;
-        if (mode == 2) {
-            // tile combine (ws_tile_combine): 64- or 32-column workgroups, 16 < M <= 128 (one 128-row
-            // instantiation: rows >= M are loaded clamped and never stored)
-#define ZK_WS_TC(NCH_)                                                                                             \
-    do {                                                                                                          \
-        if (ncw == 2) ZK_WS_LAUNCH5(2, NCH_, 8, 1, 2);                                                            \
-        else ZK_WS_LAUNCH5(2, NCH_, 8, 1, 4);                                                                     \
-    } while (0)
-            ZK_REQUIRE(ng == 1 && (ncw == 2 || ncw == 4) && N % (16 * ncw) == 0 && nsplit <= 8 &&
-                           tc_cnt && tc_x && tc_stats,
-                       "zk_gemm_resid: M=%d N=%d nsplit=%d (needs 16 < M <= 128, 32/64-column tiles, nsplit <= 8)",
-                       M, N, nsplit);
-            switch (nchunks) {
-                case 2: ZK_WS_TC(2); break;
-                case 4: ZK_WS_TC(4); break;
-                case 8: ZK_WS_TC(8); break;
-                case 16: ZK_WS_TC(16); break;
-                case 32: ZK_WS_TC(32); break;
-                default: break;
-            }
-#undef ZK_WS_TC
-        } else if (mode == 0) {
+        if (mode == 0) {
             switch (nchunks) {
                 case 2: ZK_WS_LAUNCH(0, 2); break;
                 case 4: ZK_WS_LAUNCH(0, 4); break;

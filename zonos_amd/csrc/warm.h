@@ -23,10 +23,4 @@ int zk_resid_ln_warm(const float* part, int nsplit, const void* x_in, const void
                      int rows, int D, void* x_out, void* xn_out, int ln_on_sum, const int32_t* skip, ZkWarm warm,
                      void* stream);
 int zk_gemm_bf16_warm(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, int mode, float* Cpart,
-                      void* Cout, const int32_t* skip_flag, ZkWarm warm, void* stream, int* tc_cnt = nullptr,
-                      void* tc_x = nullptr, float* tc_stats = nullptr);
-int zk_gemm_resid_warm(const void* A, long lda, const void* W, int M, int N, int K, int nsplit, float* part, void* x,
-                       float* stats, int* cnt, const int32_t* skip_flag, ZkWarm warm, void* stream);
-int zk_gemm_ln_warm(const void* x, long lda, const void* W, int M, int N, int K, int nsplit, int mode, float* Cpart,
-                    void* Cout, const void* ln_w, const void* ln_b, float eps, const float* stats, int T,
-                    const int32_t* skip_flag, ZkWarm warm, void* stream);
+                      void* Cout, const int32_t* skip_flag, ZkWarm warm, void* stream);

@@ -197,9 +197,6 @@ class HipBackbone:
         x, xn, q, y, h, part = ws["x"], ws["xn"], ws["q"], ws["y"], ws["h"], ws["part"]
         scal = ws["scal"]
         pos_dev = None if prefill else ptr(scal[1:2])
-        if not prefill and ws.get("fuse"):
-            self._layers_fused(ws, R, stream, skip)
-            return
         for i, L in enumerate(self.layers):
             kc, vt = self._kv(ws, i)
             call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), M, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip, stream)
@@ -231,64 +228,13 @@ class HipBackbone:
                  stream)
 
 
-    def _layers_fused(self, ws, R: int, stream, skip):
-        """Decode step of the blocks without k_resid_ln (16 < R <= 128): out_proj and fc2 reduce their
-        split-K slabs and add the residual in their own tail (zk_gemm_resid), in_proj / fc1 / the heads
-        apply the LayerNorm while staging the residual rows (zk_gemm_ln) -- the sequence of
-        zk_decode_step with fuse_resid (capi.cpp). Leaves the heads' logits in ws['part']."""
-        c = self.cfg
-        D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
-        Nqkv = (H + 2 * Hk) * hd
-        sp = ws["splits"]
-        x, xn, y, h, part, scal = ws["x"], ws["xn"], ws["y"], ws["h"], ws["part"], ws["scal"]
-        To, Tf = ws["fuse"]
-        for i, L in enumerate(self.layers):
-            kc, vt = self._kv(ws, i)
-            if i == 0:                       # layer 0's LayerNorm ran in the embedding kernel
-                call("zk_gemm_bf16", ptr(xn), D, ptr(L["wqkv"]), R, Nqkv, D, sp["qkv"], 0, ptr(part), None, skip,
-                     stream)
-            else:
-                call("zk_gemm_ln", ptr(x), D, ptr(L["wqkv"]), R, Nqkv, D, sp["qkv"], 0, ptr(part), None,
-                     ptr(L["ln1_w"]), ptr(L["ln1_b"]), c.eps, ptr(ws["stats_f"]), Tf, skip, stream)
-            call("zk_attn_decode_qkv_sc", ptr(part), sp["qkv"], ptr(self.freqs), ptr(kc), ptr(vt), R, H, Hk, hd,
-                 ws["smax"], 1, ptr(scal[1:2]), ptr(ws["attn_work"]), ws["attn_splits"], ptr(ws["attn_cnt"]), ptr(y),
-                 self.rope_neox, skip, stream)
-            call("zk_gemm_resid", ptr(y), H * hd, ptr(L["wo"]), R, D, H * hd, sp["o"], ptr(part), ptr(x),
-                 ptr(ws["stats_o"]), ptr(ws["cnt_o"]), skip, stream)
-            call("zk_gemm_ln", ptr(x), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, 1, None, ptr(h), ptr(L["ln2_w"]),
-                 ptr(L["ln2_b"]), c.eps, ptr(ws["stats_o"]), To, skip, stream)
-            call("zk_gemm_resid", ptr(h), Fd, ptr(L["fc2"]), R, D, Fd, sp["fc2"], ptr(part), ptr(x),
-                 ptr(ws["stats_f"]), ptr(ws["cnt_f"]), skip, stream)
-        call("zk_gemm_ln", ptr(x), D, ptr(self.heads), R, N_CB * VOCAB, D, sp["heads"], 0, ptr(part), None,
-             ptr(self.lnf_w), ptr(self.lnf_b), c.eps, ptr(ws["stats_f"]), Tf, skip, stream)
-
-    def _fuse_tiles(self, R: int, splits: dict):
-        """(To, Tf) row-statistics tiles of the fused residual path when every GEMM of the decode block
-        has its instantiation at this batch (16 < R <= 128), else None."""
-        c = self.cfg
-        if not self.fuse_resid or not (16 < R <= 128):
-            return None
-        lib = _lib.load()
-        D, H, hd, Fd = c.d_model, c.n_heads, c.head_dim, c.d_ff
-        Nqkv = (H + 2 * c.n_kv) * hd
-        To = lib.zk_gemm_resid_tiles(R, D, H * hd, splits["o"])
-        Tf = lib.zk_gemm_resid_tiles(R, D, Fd, splits["fc2"])
-        ok = (To in (32, 64) and Tf in (32, 64) and lib.zk_gemm_ln_supported(R, Nqkv, D, splits["qkv"], 0, Tf)
-              and lib.zk_gemm_ln_supported(R, 2 * Fd, D, 1, 1, To)
-              and lib.zk_gemm_ln_supported(R, N_CB * VOCAB, D, splits["heads"], 0, Tf))
-        return (To, Tf) if ok else None
-
-
 class HipDecoder(HipBackbone):
     """Owns device weights in engine layout and runs generate() on the GPU."""
 
     # B <= 8 decode (R <= 16 rows) runs each block as five launches (zk_gemv_fused: LayerNorm
     # prologues, residual epilogues, no split-K slabs) instead of seven
     small_batch_path = True
-    graph_steps = 8                 # decode steps captured per hipGraph (generate's G)
-    # 16 < 2B <= 128: out_proj / fc2 add the residual in their own tail and the next GEMM applies the
-    # LayerNorm while staging (no k_resid_ln launches; HipBackbone._layers_fused)
-    fuse_resid = True
+    graph_steps = 8                 # decode steps captured per hipGraph replay (generate's G)
     # layer 0's norm is fused into the embedding kernel (decode) / a zk_layernorm (prefill); False:
     # the subclass runs it as _prenorm (the hybrid backbone's RMS-norm / fp32-residual variants)
     embed_norm = True
@@ -328,8 +274,6 @@ class HipDecoder(HipBackbone):
             ws = self._ws
             ws["kv"].zero_()
             ws["attn_cnt"].zero_()
-            ws["cnt_o"].zero_()
-            ws["cnt_f"].zero_()
             return ws
         self.release()
         D, H, Hk, hd, Fd = c.d_model, c.n_heads, c.n_kv, c.head_dim, c.d_ff
@@ -365,10 +309,6 @@ class HipDecoder(HipBackbone):
             delayed=torch.empty(B, N_CB, Ld, dtype=torch.int64, device=dev),
             dbg=torch.empty(B, N_CB, VOCAB, dtype=f32, device=dev),
             graph=None,
-            # fused residual path (HipBackbone._layers_fused): row statistics and tile counters
-            fuse=self._fuse_tiles(R, splits),
-            stats_o=torch.zeros(R * 64 * 2, dtype=f32, device=dev), stats_f=torch.zeros(R * 64 * 2, dtype=f32, device=dev),
-            cnt_o=torch.zeros(64, dtype=i32, device=dev), cnt_f=torch.zeros(64, dtype=i32, device=dev),
         )
         self._ws = ws
         return ws
@@ -416,9 +356,7 @@ class HipDecoder(HipBackbone):
                              ws.get("attn_merge", 0), self.rope_neox, int(self._small(2 * B)), c.eps,
                              C.cast(ws["step_layers"], C.c_void_p), ptr(self.emb), ptr(self.heads), ptr(self.lnf_w),
                              ptr(self.lnf_b), ptr(self.freqs), ptr(ws["x"]), ptr(ws["xn"]), ptr(ws["y"]), ptr(ws["h"]),
-                             ptr(ws["part"]), ptr(ws["attn_work"]), ptr(ws["attn_cnt"]), ptr(ws["dbg"]), st, sp,
-                             int(ws.get("fuse") is not None), (C.c_int32 * 3)(), ptr(ws["stats_o"]),
-                             ptr(ws["stats_f"]), ptr(ws["cnt_o"]), ptr(ws["cnt_f"]))
+                             ptr(ws["part"]), ptr(ws["attn_work"]), ptr(ws["attn_cnt"]), ptr(ws["dbg"]), st, sp)
 
     def _c_decode(self, ws, B, st, sp, stream):
         call("zk_decode_step", C.byref(self._step_desc(ws, B, st, sp)), stream)
@@ -450,8 +388,7 @@ class HipDecoder(HipBackbone):
                  ptr(self.lnf_w), ptr(self.lnf_b), c.eps, ptr(ws["part"]), None, skip, stream)
         else:
             self._layers(ws, R, R, 1, False, stream, skip)
-            if not ws.get("fuse"):           # (the fused path ran the heads with norm_f while staging)
-                self._heads(ws, R, 1, stream, skip)
+            self._heads(ws, R, 1, stream, skip)
         call("zk_sample_heads", ptr(logits), nsp, C_ref(st), C_ref(sp), 0, 0, ptr(ws["dbg"]), stream)
         call("zk_sample_heads", ptr(logits), nsp, C_ref(st), C_ref(sp), 0, 1, None, stream)
         call("zk_eos_step", C_ref(st), 0, 0, stream)
@@ -555,11 +492,11 @@ class HipDecoder(HipBackbone):
             per_poll = min(per_poll, 6)
             eos_prev = ws["eos_mode"].cpu()
         graph = None
-        # steps per graph replay: a replay boundary costs 11-13 us of idle GPU (rocprofv3 kernel trace,
-        # profiles/r5_trace_gaps.txt: the gap in front of each step's first kernel), a kernel boundary
-        # inside the graph ~1 us; the steps past the last one are no-ops (every kernel tests the done
-        # word), so a poll may run up to G - 1 of them
-        G = max(g for g in range(1, min(self.graph_steps, per_poll) + 1) if per_poll % g == 0)   # G | per_poll
+        # steps per graph replay: a replay boundary leaves the GPU idle for 11-13 us (rocprofv3 kernel
+        # trace, profiles/r5_trace_gaps.txt: the gap in front of every step's first kernel), a kernel
+        # boundary inside the graph ~1 us. G divides the poll length; the steps after the last one are
+        # no-ops (every kernel tests the done word), so the final poll may run up to G - 1 of them
+        G = max(g for g in range(1, min(self.graph_steps, per_poll) + 1) if per_poll % g == 0)
         if use_graph and trace is None:
             graph = self._capture(ws, B, st, sp, stream, G)
         done_steps = 0
