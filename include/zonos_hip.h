@@ -55,6 +55,23 @@ int zk_sample_logits(const float* logits, int B, int K, int V,
                      const zk_sampling_params* sp, uint64_t seed, int step, int draw, int row_base,
                      int64_t* out, void* stream);
 
+/* zk_sample_logits with torch's GPU noise instead of the keyed stream: the [B][K][V] race noise is
+ * what `torch.empty_like(logits).exponential_(1)` returns when torch's CUDA generator holds
+ * (seed, offset) (sampling.py:26-28); stride from zk_torch_noise_policy(B*K*V, ...). The caller
+ * advances the generator by the policy's incr, as torch's own call would. */
+int zk_sample_logits_torch(const float* logits, int B, int K, int V,
+                           const int64_t* generated, int gen_stride, int gen_len, const float* rp,
+                           const zk_sampling_params* sp, uint64_t seed, uint64_t offset, int stride,
+                           int64_t* out, void* stream);
+/* out[e] = element e of torch's GPU `Tensor.exponential_(1)` over n elements whose call took the
+ * generator's Philox (seed, offset) (torch 2.10 ATen/native/hip/DistributionTemplates.h:52-91 with
+ * hiprand Philox4x32-10 and TransformationHelper.h:129-146; oracle/torch_philox.py). */
+int zk_torch_exponential(float* out, long n, uint64_t seed, uint64_t offset, int stride, void* stream);
+/* Host-only: torch's calc_execution_policy for an n-element distribution call on a device with
+ * mp_count CUs of max_threads_per_mp threads: the kernel's grid-stride (256 x grid) and the Philox
+ * offset the call consumes (DistributionTemplates.h:52-63). */
+int zk_torch_noise_policy(long n, int mp_count, int max_threads_per_mp, int* stride, long* incr);
+
 /* Delay pattern (zonos/codebook_pattern.py:5-12). codes int64 [B][K][T] ->
  * delayed int64 [B][K][T+K]; revert: delayed [B][K][L] -> codes [B][K][L-K]. */
 int zk_delay_apply(const int64_t* codes, int B, int K, int T, int64_t mask_token,
@@ -214,6 +231,16 @@ typedef struct zk_gen_state {
     int32_t B, K, Ld, V;
     uint64_t seed;
     int32_t row_base;     /* global index of utterance 0 (batch sharding) */
+    /* Noise mode. 0: the engine's keyed stream (seed, step, draw, row_base + b, codebook, token).
+     * 1: torch's own GPU stream -- the values `torch.empty_like(probs).exponential_(1)` gives the
+     * reference's sampler (sampling.py:26-28) when torch's CUDA generator holds (seed, noise_offset):
+     * sampler call c (0 = the prefill sample, model.py:304; then one per decode step, model.py:365,
+     * and one per EOS resample, model.py:388) reads the stream at Philox offset noise_offset +
+     * c * noise_incr over the [B][K][V] tensor with grid-stride noise_stride (zk_torch_noise_policy). */
+    int32_t noise_mode;
+    uint64_t noise_offset;
+    int32_t noise_stride;
+    int32_t noise_incr;
 } zk_gen_state;
 
 /* Engine sampler: logits from the heads GEMM split-K slabs part [nsplit][2B][K*V] (rows

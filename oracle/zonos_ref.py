@@ -359,7 +359,7 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
              max_new_tokens: int = 86 * 30, cfg_scale: float = 2.0, batch_size: int = 1,
              sampling_params: dict = DEFAULT_SAMPLING, seed: int = 0, row_base: int = 0,
              trace: dict | None = None, force_full_length: bool = False, max_steps_run: int | None = None,
-             force_delayed: torch.Tensor | None = None):
+             force_delayed: torch.Tensor | None = None, noise_fn=None):
     """Restatement of Zonos.generate (model.py:224-457) on CPU.
 
     Noise for sampler call (step, draw) comes from oracle.philox.exp_noise(seed, step, draw, ...):
@@ -368,7 +368,10 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
     runs max_steps (the benchmark mode). ``max_steps_run`` stops the loop early
     (CPU baseline windows). ``trace`` (optional dict) receives per-step logits/tokens.
     ``force_delayed`` (test instrumentation) overwrites every written frame with the given
-    delayed codes after it is sampled (teacher forcing on a recorded history).
+    delayed codes after it is sampled (teacher forcing on a recorded history). ``noise_fn(step,
+    draw)`` (optional) replaces the keyed stream; it is called once per sampler call that draws
+    noise (temperature > 0), in the reference's call order -- e.g. torch's own
+    `exponential_` on a generator, the reference's noise (sampling.py:26-28).
     """
     assert cfg_scale != 1, "TODO: add support for cfg_scale=1"   # model.py:247
     if batch_size * 2 != prefix_conditioning.shape[0]:
@@ -391,6 +394,10 @@ def generate(W, cfg: BackboneCfg, prefix_conditioning: torch.Tensor, audio_prefi
     delayed = apply_delay(codes, MASK)
 
     def noise(step, draw):
+        if not float(sp.get("temperature", 1.0)) > 0:
+            return None                     # greedy: the reference draws no noise (sampling.py:325-326)
+        if noise_fn is not None:
+            return noise_fn(step, draw)
         return torch.from_numpy(exp_noise(seed, step, draw, B, cfg.n_cb, cfg.vocab, row_base))
 
     ids = delayed[..., :P + 1].repeat(2, 1, 1)

@@ -171,6 +171,7 @@ def test_ctypes_struct_layouts_match_the_c_abi(lib):
     for which, cls in [(0, _lib.SamplingParams), (1, _lib.GenState), (4, ZkCondSeg), (5, ZkCondPlan)]:
         assert lib.zk_abi_size(which) == C.sizeof(cls), (cls.__name__, lib.zk_abi_size(which), C.sizeof(cls))
     assert lib.zk_abi_size(12) == _lib.GenState.seed.offset
+    assert lib.zk_abi_size(22) == _lib.GenState.noise_offset.offset
     assert lib.zk_abi_size(6) == C.sizeof(_lib.StepLayer) and lib.zk_abi_size(7) == C.sizeof(_lib.StepDesc)
     assert lib.zk_abi_size(13) == _lib.StepDesc.eps.offset
     assert lib.zk_abi_size(14) == _lib.StepDesc.st.offset and lib.zk_abi_size(15) == _lib.StepDesc.sp.offset

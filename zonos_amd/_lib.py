@@ -32,7 +32,8 @@ class GenState(C.Structure):
     _fields_ = [("scal", P), ("eos_mode", P), ("steps_after", P), ("remaining", P), ("stopping", P),
                 ("act", P), ("rp", P), ("tok0", P), ("tok1", P), ("delayed", P),
                 ("B", C.c_int32), ("K", C.c_int32), ("Ld", C.c_int32), ("V", C.c_int32),
-                ("seed", U64), ("row_base", C.c_int32)]
+                ("seed", U64), ("row_base", C.c_int32), ("noise_mode", C.c_int32), ("noise_offset", U64),
+                ("noise_stride", C.c_int32), ("noise_incr", C.c_int32)]
 
 
 class StepLayer(C.Structure):
@@ -89,6 +90,8 @@ _SIGS = {
     "zk_version": [],
     "zk_device_sync": [],
     "zk_sample_logits": [P, I, I, I, P, I, I, P, C.POINTER(SamplingParams), U64, I, I, I, P, P],
+    "zk_sample_logits_torch": [P, I, I, I, P, I, I, P, C.POINTER(SamplingParams), U64, U64, I, P, P],
+    "zk_torch_exponential": [P, L, U64, U64, I, P],
     "zk_delay_apply": [P, I, I, I, I64, P, P],
     "zk_delay_revert": [P, I, I, I, P, P],
     "zk_embed_codes": [P, I, I, I, L, L, P, I, P, I, I, I, P, I, I, P, P, F, P, P, P],
@@ -174,13 +177,16 @@ def load():
     lib.zk_dac_resunit_supported.argtypes = [I]
     lib.zk_gemm_warm_tiles.restype = C.c_int
     lib.zk_gemm_warm_tiles.argtypes = [I, I, I, I, I, I]
+    lib.zk_torch_noise_policy.restype = C.c_int
+    lib.zk_torch_noise_policy.argtypes = [L, I, I, C.POINTER(C.c_int), C.POINTER(C.c_long)]
     _lib = lib
     return lib
 
 
 def exported_symbols() -> list[str]:
     return list(_SIGS) + ["zk_last_error", "zk_loudness_max_blocks", "zk_abi_size",
-                          "zk_dac_decode_workspace", "zk_dac_resunit_supported", "zk_gemm_warm_tiles"]
+                          "zk_dac_decode_workspace", "zk_dac_resunit_supported", "zk_gemm_warm_tiles",
+                          "zk_torch_noise_policy"]
 
 
 def call(name: str, *args):

@@ -46,6 +46,7 @@ extern "C" long zk_abi_size(int which) {
         case 19: return (long)sizeof(zk_hybrid_desc);
         case 20: return (long)offsetof(zk_hybrid_desc, st);
         case 21: return (long)offsetof(zk_hybrid_desc, eps);
+        case 22: return (long)offsetof(zk_gen_state, noise_offset);
         default: return -1;
     }
 }

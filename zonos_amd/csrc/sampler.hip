@@ -47,6 +47,37 @@ ZK_DEV float exp_noise(uint64_t seed, int step, int draw, int row, int cb, int v
     return (float)(-log(u));
 }
 
+// All four Philox4x32-10 output words (the same rounds as philox_w0).
+ZK_DEV uint4 philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return uint4{c0, c1, c2, c3};
+}
+
+// Element e of torch's GPU `Tensor.exponential_(1)` over a tensor whose call took Philox
+// (seed, offset) and ran with grid-stride `stride` (oracle/torch_philox.py; torch 2.10
+// ATen/native/hip/DistributionTemplates.h:52-91, rocrand_philox4x32_10.h, rocrand_uniform.h:66-68,
+// ATen/core/TransformationHelper.h:129-146): thread t = e % stride of iteration j = (e / stride) / 4
+// draws Philox(counter (offset / 4 + j, t), key seed) and takes word (e / stride) % 4.
+ZK_DEV float torch_exp_noise(uint64_t seed, uint64_t offset, long e, int stride) {
+    const long t = e % stride, q = e / stride;
+    const uint64_t ctr = offset / 4 + (uint64_t)(q >> 2);
+    const uint4 r = philox4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, (uint32_t)(t >> 32), (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
+    const int ii = (int)(q & 3);
+    const uint32_t w = ii == 0 ? r.x : ii == 1 ? r.y : ii == 2 ? r.z : r.w;
+    const float u = 2.3283064e-10f + (float)w * 2.3283064e-10f;       // hiprand_uniform4: (0, 1]
+    // torch: log = u >= 1 - eps/2 ? -eps/2 : __logf(u) (ATen/NumericUtils.h:150-160); q = -1 / 1 * log
+    const float lg = u >= 1.0f - 5.96046448e-08f ? -5.96046448e-08f : __builtin_logf(u);
+    return -1.0f * lg;
+}
+
 struct Smem {
     float key[SORTN];
     int idx[SORTN];
@@ -206,6 +237,11 @@ struct RowCtx {
     float rp;
     int step, draw, row;
     uint64_t seed;
+    // torch noise mode (nstride > 0): torch's exponential_ stream of the call at Philox offset
+    // `noff`, this row's elements starting at `ebase` of the [B][K][V] noise tensor
+    uint64_t noff;
+    int nstride;
+    long ebase;
 };
 
 // Everything after the logits are in registers: rep-penalty, shaping, race / argmax.
@@ -266,7 +302,9 @@ ZK_DEV int sample_row(float* x, const RowCtx& c, const zk_sampling_params& sp, S
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
         const int v = threadIdx.x + NT * i;
-        if (v < V) x[i] = __fdiv_rn(x[i], exp_noise(c.seed, c.step, c.draw, c.row, c.k, v));
+        if (v < V)
+            x[i] = __fdiv_rn(x[i], c.nstride > 0 ? torch_exp_noise(c.seed, c.noff, c.ebase + v, c.nstride)
+                                                 : exp_noise(c.seed, c.step, c.draw, c.row, c.k, v));
     }
     return block_argmax(x, V, s);
 }
@@ -274,7 +312,8 @@ ZK_DEV int sample_row(float* x, const RowCtx& c, const zk_sampling_params& sp, S
 __global__ __launch_bounds__(NT) void k_sample_logits(const float* logits, int B, int K, int V,
                                                       const int64_t* gen, int gen_stride, int gen_len,
                                                       const float* rp, zk_sampling_params sp, uint64_t seed,
-                                                      int step, int draw, int row_base, int64_t* out) {
+                                                      int step, int draw, int row_base, uint64_t noff, int nstride,
+                                                      int64_t* out) {
     __shared__ Smem s;
     const int b = blockIdx.x / K, k = blockIdx.x % K;
     float x[NPT];
@@ -285,7 +324,7 @@ __global__ __launch_bounds__(NT) void k_sample_logits(const float* logits, int B
         x[i] = v < V ? row[v] : -INFINITY;
     }
     RowCtx c{b, k, V, gen ? gen + ((size_t)b * K + k) * gen_stride : nullptr, gen_len,
-             rp ? rp[b] : 1.f, step, draw, row_base + b, seed};
+             rp ? rp[b] : 1.f, step, draw, row_base + b, seed, noff, nstride, ((long)b * K + k) * V};
     const int t = sample_row(x, c, sp, s);
     if (threadIdx.x == 0) out[(size_t)b * K + k] = t;
 }
@@ -302,7 +341,7 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
     // the done word, the step scalars, this row's state and the logits; the finished check comes
     // after them (the loads are in bounds either way).
     const int done = scal[3];
-    const int offset = scal[0], step = scal[2];
+    const int offset = scal[0], step = scal[2], nres = scal[4];
     const float rpb = st.rp[b];
     const int actb = st.act[b];
     int new_eos_b = 0;
@@ -371,8 +410,14 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
             if (k == 0 && sp.force_full_length) x[i] = -INFINITY;              // benchmark mode
         }
     }
+    // torch noise mode: the reference's sampler calls so far -- the prefill sample, one per earlier
+    // decode step (scal[2] starts at 1) and one per earlier EOS resample (scal[4]) -- each took
+    // noise_incr of the generator's Philox offset (model.py:304,365,388)
+    const long call = prefill ? 0 : (long)step + nres + draw;
     RowCtx c{b, k, V, prefill ? nullptr : st.delayed + ((size_t)b * K + k) * st.Ld, offset,
-             prefill ? 1.f : rpb, prefill ? 0 : step, draw, st.row_base + b, st.seed};
+             prefill ? 1.f : rpb, prefill ? 0 : step, draw, st.row_base + b, st.seed,
+             st.noise_offset + (uint64_t)call * (uint64_t)st.noise_incr, st.noise_mode ? st.noise_stride : 0,
+             ((long)(st.row_base + b) * K + k) * V};
     const int t = sample_row(x, c, sp, s);
     if (threadIdx.x == 0) (draw ? st.tok1 : st.tok0)[b * K + k] = t;
 }
@@ -476,8 +521,49 @@ extern "C" int zk_sample_logits(const float* logits, int B, int K, int V, const 
     ZK_REQUIRE(sp != nullptr, "zk_sample_logits: null params");
     ZK_REQUIRE(sp->top_k >= 0 && sp->rp_window >= 0, "zk_sample_logits: negative top_k/window");
     hipLaunchKernelGGL(k_sample_logits, dim3(B * K), dim3(NT), 0, (hipStream_t)stream, logits, B, K, V,
-                       generated, gen_stride, gen_len, rp, *sp, seed, step, draw, row_base, out);
+                       generated, gen_stride, gen_len, rp, *sp, seed, step, draw, row_base, (uint64_t)0, 0, out);
     ZK_CHECK_LAUNCH("zk_sample_logits");
+    return 0;
+}
+
+extern "C" int zk_sample_logits_torch(const float* logits, int B, int K, int V, const int64_t* generated,
+                                      int gen_stride, int gen_len, const float* rp, const zk_sampling_params* sp,
+                                      uint64_t seed, uint64_t offset, int stride, int64_t* out, void* stream) {
+    ZK_REQUIRE(V > 0 && V <= NT * NPT, "zk_sample_logits_torch: V=%d must be in (0, %d]", V, NT * NPT);
+    ZK_REQUIRE(B > 0 && K > 0, "zk_sample_logits_torch: empty batch");
+    ZK_REQUIRE(sp != nullptr, "zk_sample_logits_torch: null params");
+    ZK_REQUIRE(sp->top_k >= 0 && sp->rp_window >= 0, "zk_sample_logits_torch: negative top_k/window");
+    ZK_REQUIRE(stride > 0 && stride % 256 == 0, "zk_sample_logits_torch: stride %d (256 x grid)", stride);
+    hipLaunchKernelGGL(k_sample_logits, dim3(B * K), dim3(NT), 0, (hipStream_t)stream, logits, B, K, V,
+                       generated, gen_stride, gen_len, rp, *sp, seed, 0, 0, 0, offset, stride, out);
+    ZK_CHECK_LAUNCH("zk_sample_logits_torch");
+    return 0;
+}
+
+namespace {
+__global__ void k_torch_exponential(float* out, long n, uint64_t seed, uint64_t offset, int stride) {
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x)
+        out[e] = torch_exp_noise(seed, offset, e, stride);
+}
+}  // namespace
+
+extern "C" int zk_torch_exponential(float* out, long n, uint64_t seed, uint64_t offset, int stride, void* stream) {
+    ZK_REQUIRE(n >= 0 && out != nullptr, "zk_torch_exponential: bad output");
+    ZK_REQUIRE(stride > 0 && stride % 256 == 0, "zk_torch_exponential: stride %d (256 x grid)", stride);
+    if (n == 0) return 0;
+    const int grid = (int)std::min<long>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_torch_exponential, dim3(grid), dim3(256), 0, (hipStream_t)stream, out, n, seed, offset,
+                       stride);
+    ZK_CHECK_LAUNCH("zk_torch_exponential");
+    return 0;
+}
+
+extern "C" int zk_torch_noise_policy(long n, int mp_count, int max_threads_per_mp, int* stride, long* incr) {
+    ZK_REQUIRE(n > 0 && mp_count > 0 && max_threads_per_mp >= 256 && stride && incr,
+               "zk_torch_noise_policy: n=%ld mp=%d max_threads=%d", n, mp_count, max_threads_per_mp);
+    const long grid = std::min<long>((long)mp_count * (max_threads_per_mp / 256), (n + 255) / 256);
+    *stride = (int)(256 * grid);
+    *incr = ((n - 1) / (256 * grid * 4) + 1) * 4;
     return 0;
 }
 

@@ -234,7 +234,7 @@ class HipDecoder(HipBackbone):
     # B <= 8 decode (R <= 16 rows) runs each block as five launches (zk_gemv_fused: LayerNorm
     # prologues, residual epilogues, no split-K slabs) instead of seven
     small_batch_path = True
-    graph_steps = 8                 # decode steps captured per hipGraph replay (generate's G)
+    graph_steps = 1                 # decode steps captured per hipGraph replay (generate's G; 8 measured no faster)
     # layer 0's norm is fused into the embedding kernel (decode) / a zk_layernorm (prefill); False:
     # the subclass runs it as _prenorm (the hybrid backbone's RMS-norm / fp32-residual variants)
     embed_norm = True
@@ -331,10 +331,11 @@ class HipDecoder(HipBackbone):
         call("zk_gemm_bf16", ptr(last), S * D, ptr(self.heads), R, N_CB * VOCAB, D, ws["splits"]["heads"], 0,
              ptr(ws["part"]), None, skip, stream)
 
-    def _gen_state(self, ws, B, seed, row_base) -> GenState:
+    def _gen_state(self, ws, B, seed, row_base, noise=(0, 0, 0, 0)) -> GenState:
+        """noise = (mode, Philox offset, grid-stride, offset per call): zk_gen_state's noise words."""
         return GenState(ptr(ws["scal"]), ptr(ws["eos_mode"]), ptr(ws["steps_after"]), ptr(ws["remaining"]),
                         ptr(ws["stopping"]), ptr(ws["act"]), ptr(ws["rp"]), ptr(ws["tok0"]), ptr(ws["tok1"]),
-                        ptr(ws["delayed"]), B, N_CB, ws["Ld"], VOCAB, seed & 0xFFFFFFFFFFFFFFFF, row_base)
+                        ptr(ws["delayed"]), B, N_CB, ws["Ld"], VOCAB, seed & 0xFFFFFFFFFFFFFFFF, row_base, *noise)
 
     # the step's launch sequence is enqueued by the C ABI (zk_decode_step); False runs the same
     # sequence from Python (bit-identical; kept as the reference for the test)
@@ -402,8 +403,15 @@ class HipDecoder(HipBackbone):
                  cfg_scale: float = 2.0, batch_size: int = 1, sampling_params: dict | None = None,
                  seed: int = 0, row_base: int = 0, force_full_length: bool = False, callback=None,
                  progress=None, poll_every: int = 16, trace: dict | None = None, use_graph: bool = True,
-                 _after_prefill=None):
+                 _after_prefill=None, noise: str = "keyed", generator: torch.Generator | None = None):
         """Zonos.generate (model.py:224-457). Returns the list of int64 [9, T_i] code tensors.
+
+        ``noise`` picks the race noise of the sampler: "keyed" = the engine's stream keyed by
+        (seed, step, draw, row_base + b, codebook, token), independent of batch sharding; "torch" =
+        torch's own GPU stream, the values the reference's `exponential_` draws from ``generator``
+        (default: torch's CUDA generator of the device) -- the generator is read at the start and
+        advanced by the Philox offset the reference's sampler calls would have consumed, so
+        ``torch.manual_seed(s)`` followed by this call leaves torch's RNG where the reference leaves it.
 
         ``trace`` (optional dict) receives per-step fp32 CFG logits (before bias) and the
         sampled frames -- test instrumentation, forces one step per poll and no graph."""
@@ -437,7 +445,18 @@ class HipDecoder(HipBackbone):
         sp = SamplingParams(float(spd["temperature"]), float(spd["top_p"]), float(spd["min_p"]),
                             float(spd["linear"]), float(spd["conf"]), float(spd["quad"]), int(spd["top_k"]),
                             int(spd["repetition_penalty_window"]), float(cfg_scale), int(force_full_length))
-        st = self._gen_state(ws, B, seed, row_base)
+        gen = None
+        if noise == "torch":
+            if row_base:
+                raise ValueError("noise='torch' is one process's stream (row_base must be 0)")
+            gen = generator if generator is not None else torch.cuda.default_generators[self.device.index or 0]
+            seed, off0 = int(gen.initial_seed()), int(gen.get_offset())
+            stride, incr = zsampling.torch_noise_policy(B * N_CB * VOCAB, self.device)
+            st = self._gen_state(ws, B, seed, 0, (1, off0, stride, incr))
+        elif noise == "keyed":
+            st = self._gen_state(ws, B, seed, row_base)
+        else:
+            raise ValueError(f"noise must be 'keyed' or 'torch', not {noise!r}")
         ws["scal"].zero_()
 
         # ---- prefill (model.py:297-319, _prefill 181-202)
@@ -493,7 +512,7 @@ class HipDecoder(HipBackbone):
             eos_prev = ws["eos_mode"].cpu()
         graph = None
         # steps per graph replay: a replay boundary leaves the GPU idle for 11-13 us (rocprofv3 kernel
-        # trace, profiles/r5_trace_gaps.txt: the gap in front of every step's first kernel), a kernel
+        # trace, profiles/r5_trace_gaps_c{2,3}.txt: the gap before every step's first kernel), a kernel
         # boundary inside the graph ~1 us. G divides the poll length; the steps after the last one are
         # no-ops (every kernel tests the done word), so the final poll may run up to G - 1 of them
         G = max(g for g in range(1, min(self.graph_steps, per_poll) + 1) if per_poll % g == 0)
@@ -531,7 +550,12 @@ class HipDecoder(HipBackbone):
                 trace["tokens"].append(ws["delayed"][..., off:off + 1].clone())
             if int(scal[3]):
                 break
-        offset = int(ws["scal"][0].item()) - 1
+        scal = ws["scal"].cpu()
+        offset = int(scal[0]) - 1
+        if gen is not None and float(spd["temperature"]) > 0:
+            # sampler calls the reference made: the prefill sample, one per loop iteration
+            # (scal[2] counts from 1) and one per EOS resample (scal[4]); greedy draws nothing
+            gen.set_offset(off0 + (int(scal[2]) + int(scal[4])) * incr)
         if trace is not None:
             trace["delayed"] = ws["delayed"].clone()
             trace["offset"] = offset

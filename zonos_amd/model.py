@@ -115,10 +115,14 @@ class Zonos:
                  callback: Callable[[torch.Tensor, int, int], bool] | None = None, *, seed: int | None = None,
                  row_base: int = 0, force_full_length: bool = False):
         """model.py:224-457. ``disable_torch_compile`` is accepted and ignored (the step is a
-        captured hipGraph). ``seed`` keys the sampling noise; by default it is drawn from
-        torch's global generator so ``torch.manual_seed`` makes runs reproducible."""
-        if seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        captured hipGraph). Sampling noise: by default (``seed`` None) the reference's own -- every
+        sampler call takes the values `torch.empty_like(probs).exponential_(1)` would draw from torch's
+        CUDA generator (sampling.py:26-28) and advances that generator as the reference does, so
+        ``torch.manual_seed(s)`` (sample.py:19) gives the reference's noise on the same GPU. An
+        integer ``seed`` selects the engine's keyed stream instead (independent of batch sharding)."""
+        noise = "torch" if seed is None else "keyed"
+        if noise == "torch" and row_base:
+            raise ValueError("row_base needs an explicit seed (the keyed noise stream)")
         prog = None
         if progress_bar:
             try:
@@ -129,8 +133,9 @@ class Zonos:
             except ImportError:
                 prog = None
         out = self.engine.generate(prefix_conditioning.to(self.device), audio_prefix_codes, max_new_tokens,
-                                   cfg_scale, batch_size, sampling_params, seed=seed, row_base=row_base,
-                                   force_full_length=force_full_length, callback=callback, progress=prog)
+                                   cfg_scale, batch_size, sampling_params, seed=seed or 0, row_base=row_base,
+                                   force_full_length=force_full_length, callback=callback, progress=prog,
+                                   noise=noise)
         if prog is not None:
             prog.close()
         return out

@@ -1,5 +1,8 @@
-"""sample_from_logits on the GPU (zonos/sampling.py:232-328), same signature plus the
-noise-stream key (seed, step, draw, row_base); see oracle/philox.py for the stream.
+"""sample_from_logits on the GPU (zonos/sampling.py:232-328), same signature. The race noise is
+the reference's own by default: the values `torch.empty_like(probs).exponential_(1)` draws from
+torch's CUDA generator (or ``generator=``), which is then advanced exactly as that call advances
+it (oracle/torch_philox.py). Passing ``seed=`` selects the engine's keyed stream instead, keyed by
+(seed, step, draw, row_base); see oracle/philox.py.
 
 Also the reference's sampling loggers (sampling.py:5-9): ``zonos.sampling`` (DEBUG: the
 sampling parameters once, then probability statistics of utterance 0 / codebook 0 every 64th
@@ -35,8 +38,8 @@ def sample_from_logits(logits: torch.Tensor, temperature: float = 1.0, top_p: fl
                        min_p: float = 0.0, linear: float = 0.0, conf: float = 0.0, quad: float = 0.0,
                        generated_tokens: torch.Tensor | None = None,
                        repetition_penalty: float | torch.Tensor = 3.0, repetition_penalty_window: int = 2,
-                       eos_token_id: int = -1, *, seed: int = 0, step: int = 0, draw: int = 0,
-                       row_base: int = 0) -> torch.Tensor:
+                       eos_token_id: int = -1, *, seed: int | None = None, step: int = 0, draw: int = 0,
+                       row_base: int = 0, generator: torch.Generator | None = None) -> torch.Tensor:
     _lib.require_gpu(logits, "logits")
     lg = logits.float().contiguous()
     B, K, V = lg.shape
@@ -57,10 +60,32 @@ def sample_from_logits(logits: torch.Tensor, temperature: float = 1.0, top_p: fl
                                           repetition_penalty_window=repetition_penalty_window),
                            None if gen is None else gen[0, 0], float(rp[0]), eos_token_id)
     out = torch.empty(B, K, 1, dtype=torch.int64, device=lg.device)
-    call("zk_sample_logits", ptr(lg), B, K, V, ptr(gen), gen_len, gen_len, ptr(rp), _lib.C.byref(sp),
-         int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(draw), int(row_base), ptr(out),
-         _lib.stream_ptr(lg.device))
+    if seed is not None:
+        call("zk_sample_logits", ptr(lg), B, K, V, ptr(gen), gen_len, gen_len, ptr(rp), _lib.C.byref(sp),
+             int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(draw), int(row_base), ptr(out),
+             _lib.stream_ptr(lg.device))
+        return out
+    g = generator if generator is not None else torch.cuda.default_generators[lg.device.index or 0]
+    stride, incr = torch_noise_policy(B * K * V, lg.device)
+    off = int(g.get_offset())
+    call("zk_sample_logits_torch", ptr(lg), B, K, V, ptr(gen), gen_len, gen_len, ptr(rp), _lib.C.byref(sp),
+         int(g.initial_seed()) & 0xFFFFFFFFFFFFFFFF, off, stride, ptr(out), _lib.stream_ptr(lg.device))
+    if temperature > 0:                  # greedy decoding draws no noise (sampling.py:325-326)
+        g.set_offset(off + incr)
     return out
+
+
+def torch_noise_policy(n: int, device) -> tuple[int, int]:
+    """(grid-stride, Philox offset increment) of torch's `exponential_` over n elements on
+    ``device`` (zk_torch_noise_policy: DistributionTemplates.h calc_execution_policy)."""
+    p = torch.cuda.get_device_properties(device)
+    stride, incr = _lib.C.c_int(), _lib.C.c_long()
+    rc = _lib.load().zk_torch_noise_policy(int(n), int(p.multi_processor_count),
+                                           int(p.max_threads_per_multi_processor), _lib.C.byref(stride),
+                                           _lib.C.byref(incr))
+    if rc != 0:
+        raise _lib.ZonosHipError(f"zk_torch_noise_policy failed: {_lib.load().zk_last_error().decode()}")
+    return stride.value, incr.value
 
 
 # ---------------------------------------------------------------- debug statistics (host side)
