@@ -1,13 +1,14 @@
 """Fixture of torch's own GPU `Tensor.exponential_(1)` stream -> tests/golden/torch_exp_noise.npz.
 
-Runs on the GPU box (torch only; no reference code involved):
-    python tests/golden/make_torch_noise.py
+Runs on the GPU box (torch only; no reference code involved), then copy the file here:
+    python tests/golden/make_torch_noise.py gpurun_out/torch_exp_noise.npz
 It pins oracle/torch_philox.py (the CPU restatement of that stream, tests/test_torch_noise_cpu.py):
 for each case the generator's (seed, offset) before the call, its offset after, and the values --
 every value for the small tensors, 4096 evenly spaced ones for the [64][9][1026] and [300][9][1026]
 tensors (the grid-capped and the two-iteration cases of torch's grid-stride kernel).
 """
 import os
+import sys
 
 import numpy as np
 import torch
@@ -37,7 +38,7 @@ def main():
             out[f"c{i}_q"] = q[idx].astype(np.float32)
             i += 1
     out["n_cases"] = np.int64(i)
-    np.savez_compressed(os.path.join(HERE, "torch_exp_noise.npz"), **out)
+    np.savez_compressed(sys.argv[1] if len(sys.argv) > 1 else os.path.join(HERE, "torch_exp_noise.npz"), **out)
     print(f"{i} cases; mp {p.multi_processor_count} max_threads {p.max_threads_per_multi_processor}")
 
 

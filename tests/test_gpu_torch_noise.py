@@ -87,6 +87,22 @@ def test_sample_from_logits_default_is_the_reference_stream():
     assert int(g.get_offset()) == off0
 
 
+def _eos_near_tie(tr, tau) -> bool:
+    """Some codebook-0 draw of the oracle's run, on a row that has not stopped yet (model.py:399-402:
+    later EOS decisions of a stopped row change nothing), has EOS among its top two with a margin
+    <= tau."""
+    stopped = torch.zeros(tr["tokens"][0].shape[0], dtype=torch.bool)
+    for dec, tok in zip(tr["decision"], tr["tokens"]):
+        for kind, arr in dec:
+            top = arr[:, 0].topk(2, dim=-1)
+            m = torch.log(top.values[:, 0] / top.values[:, 1].clamp_min(1e-38))
+            eos = (top.indices == 1024).any(dim=-1)
+            if bool((eos & (m <= tau) & ~stopped).any()):
+                return True
+        stopped |= tok[:, 0, 0] == 1024
+    return False
+
+
 @pytest.mark.parametrize("name", ["sampled_cli", "eos_sampled", "sampled_knobs"])
 def test_generate_reference_noise_teacher_forced(name):
     """generate() with the reference's noise (Zonos.generate's default): the oracle's generate (the
@@ -97,23 +113,32 @@ def test_generate_reference_noise_teacher_forced(name):
     the same offset (the same number of sampler calls, EOS resamples included)."""
     c = load_gen_case(name)
     B = c["B"]
-    g = torch.Generator(device=DEV)
-    g.manual_seed(4321)
-    calls = []
-
-    def noise_fn(step, draw):
-        calls.append((step, draw))
-        return torch.empty(B, 9, 1026, device=DEV).exponential_(1, generator=g).cpu()
-
-    tr = {}
-    zonos_ref.generate(c["W"], c["cfg"], c["cond"], c["prefix"], c["max_new"], 2.0, B, c["sp"], trace=tr,
-                       noise_fn=noise_fn)
-    off_ref = int(g.get_offset())
-    gold = tr["delayed"].long()
-    P = c["prefix"].shape[2]
     sp = c["sp"]
     gain = (sp["linear"] + np.log(1026) * sp["conf"]) if sp["linear"] > 0 else 1.0
     tau_ratio = TAU_LOGRATIO * max(1.0, gain) / max(sp["temperature"], 1e-6)
+    # A codebook-0 decision between EOS and another token whose margin is within the tolerance may
+    # go either way on the GPU; it changes that row's EOS state and the number of sampler calls
+    # (a resample), i.e. the noise of every later step. Use the first generator seed whose
+    # reference run has no such decision, so every step stays comparable.
+    for seed in range(4321, 4521):
+        g = torch.Generator(device=DEV)
+        g.manual_seed(seed)
+        calls = []
+
+        def noise_fn(step, draw):
+            calls.append((step, draw))
+            return torch.empty(B, 9, 1026, device=DEV).exponential_(1, generator=g).cpu()
+
+        tr = {}
+        zonos_ref.generate(c["W"], c["cfg"], c["cond"], c["prefix"], c["max_new"], 2.0, B, sp, trace=tr,
+                           noise_fn=noise_fn)
+        if not _eos_near_tie(tr, tau_ratio):
+            break
+    else:
+        pytest.fail("no generator seed without an EOS near-tie")
+    off_ref = int(g.get_offset())
+    gold = tr["delayed"].long()
+    P = c["prefix"].shape[2]
     stats = dict(checked=0, skipped=0, mismatch=[])
 
     def check(frame, step):
@@ -134,7 +159,7 @@ def test_generate_reference_noise_teacher_forced(name):
         frame.copy_(exp.to(frame.device))
 
     g2 = torch.Generator(device=DEV)
-    g2.manual_seed(4321)
+    g2.manual_seed(seed)
     eng = _engine(c["W"], c["cfg"])
     eng.generate(c["cond"].cuda(), c["prefix"].cuda(), c["max_new"], 2.0, B, sp, noise="torch", generator=g2,
                  callback=lambda f, s, n: (check(f, s), True)[1], _after_prefill=lambda f: check(f, 0))
@@ -142,7 +167,7 @@ def test_generate_reference_noise_teacher_forced(name):
     allowed = stats["checked"] // 200 if thresholds else 0
     assert len(stats["mismatch"]) <= allowed, stats["mismatch"][:10]
     frac = stats["skipped"] / (stats["checked"] + stats["skipped"])
-    print(name, len(calls), "sampler calls;", {k: (v if k != "mismatch" else len(v)) for k, v in stats.items()})
+    print(name, "seed", seed, len(calls), "sampler calls;", {k: (v if k != "mismatch" else len(v)) for k, v in stats.items()})
     assert frac <= 0.5, frac
     assert int(g2.get_offset()) == off_ref, (int(g2.get_offset()), off_ref, len(calls))
 

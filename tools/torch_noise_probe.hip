@@ -8,6 +8,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+extern "C" __device__ float __ocml_native_log_f32(float);
+extern "C" __device__ float __ocml_log_f32(float);
+extern "C" __device__ float __ocml_native_log2_f32(float);
+
 namespace {
 __device__ uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
@@ -32,10 +36,20 @@ __global__ void k_probe(float* out, long n, uint64_t seed, uint64_t off, int str
         const uint32_t w = (q & 3) == 0 ? r.x : (q & 3) == 1 ? r.y : (q & 3) == 2 ? r.z : r.w;
         const float u = 2.3283064e-10f + (float)w * 2.3283064e-10f;
         float lg;
+        const float y = __builtin_amdgcn_logf(u);
         if (variant == 0) lg = __builtin_logf(u);
-        else if (variant == 1) lg = __builtin_amdgcn_logf(u) * 0.693147182f;
+        else if (variant == 1) lg = y * 0.693147182f;
         else if (variant == 2) lg = (float)log((double)u);
-        else lg = __logf(u);
+        else if (variant == 3) lg = __logf(u);
+        else if (variant == 4) lg = y * __builtin_bit_cast(float, 0x3f317217u);
+        else if (variant == 5) lg = (float)((double)y * 0.6931471805599453);
+        else if (variant == 6) lg = __ocml_native_log_f32(u);
+        else if (variant == 7) lg = __ocml_log_f32(u);
+        else if (variant == 8) lg = __ocml_native_log2_f32(u) * 0.693147182f;
+        else {                                     // y * ln2 with ln2 split hi + lo (fma)
+            const float ch = __builtin_bit_cast(float, 0x3f317218u), cl = __builtin_bit_cast(float, 0xb102e308u);
+            lg = __builtin_fmaf(y, ch, y * cl);
+        }
         const float l = u >= 1.0f - 5.96046448e-08f ? -5.96046448e-08f : lg;
         out[e] = -1.0f * l;
     }

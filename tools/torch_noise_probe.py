@@ -22,26 +22,36 @@ def policy(n: int, mp: int, maxthr: int):
 
 
 def main():
-    lib = ctypes.CDLL(os.path.join(HERE, "torch_noise_probe.so"))
-    lib.probe_noise.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
-                                ctypes.c_int]
+    libs = []
+    for name, f in (("p", "torch_noise_probe.so"), ("f", "torch_noise_probe_fast.so")):
+        lib = ctypes.CDLL(os.path.join(HERE, f))
+        lib.probe_noise.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                    ctypes.c_int]
+        libs.append((name, lib))
     p = torch.cuda.get_device_properties(0)
     mp, maxthr = p.multi_processor_count, p.max_threads_per_multi_processor
     print(f"multi_processor_count {mp} max_threads_per_multi_processor {maxthr}")
     g = torch.Generator(device="cuda")
-    for seed in (0, 421, 2 ** 40 + 7):
+    for seed in (0, 421):
         g.manual_seed(seed)
-        for n in (17, 9 * 1026, 3 * 9 * 1026, 64 * 9 * 1026, 300 * 9 * 1026):
+        for n in (9 * 1026, 64 * 9 * 1026):
             off = g.get_offset()
             ref = torch.empty(n, device="cuda").exponential_(1, generator=g)
             stride, incr = policy(n, mp, maxthr)
             line = f"seed {seed} n {n} off {off} -> {g.get_offset()} (policy incr {incr}, stride {stride}):"
-            for v in range(4):
-                out = torch.empty(n, device="cuda")
-                assert lib.probe_noise(out.data_ptr(), n, seed, off, stride, v) == 0
-                bad = (out.view(torch.int32) != ref.view(torch.int32))
-                ulp = (out.view(torch.int32) - ref.view(torch.int32)).abs().max().item()
-                line += f" v{v} {int(bad.sum())} diff (max {ulp} ulp)"
+            for name, lb in libs:
+                for v in range(10):
+                    out = torch.empty(n, device="cuda")
+                    assert lb.probe_noise(out.data_ptr(), n, seed, off, stride, v) == 0
+                    bad = (out.view(torch.int32) != ref.view(torch.int32))
+                    ulp = (out.view(torch.int32) - ref.view(torch.int32)).abs().max().item()
+                    line += f" {name}{v} {int(bad.sum())}/{ulp}"
+                    if name == "p" and v == 1 and n > 100000 and seed == 0:
+                        u = torch.exp(-out[bad].double())
+                        h = torch.histc(u, bins=10, min=0, max=1).long().tolist()
+                        hu = torch.histc(torch.exp(-out.double()), bins=10, min=0, max=1).long().tolist()
+                        print("  v1 mismatch u-deciles", h, "of", hu)
+                        print("  sample mismatches (ours, torch):", list(zip(out[bad][:6].tolist(), ref[bad][:6].tolist())))
             print(line, flush=True)
 
 

@@ -73,8 +73,14 @@ ZK_DEV float torch_exp_noise(uint64_t seed, uint64_t offset, long e, int stride)
     const int ii = (int)(q & 3);
     const uint32_t w = ii == 0 ? r.x : ii == 1 ? r.y : ii == 2 ? r.z : r.w;
     const float u = 2.3283064e-10f + (float)w * 2.3283064e-10f;       // hiprand_uniform4: (0, 1]
-    // torch: log = u >= 1 - eps/2 ? -eps/2 : __logf(u) (ATen/NumericUtils.h:150-160); q = -1 / 1 * log
-    const float lg = u >= 1.0f - 5.96046448e-08f ? -5.96046448e-08f : __builtin_logf(u);
+    // torch: log = u >= 1 - eps/2 ? -eps/2 : __logf(u) (ATen/NumericUtils.h:150-160); q = -1 / 1 * log.
+    // torch's __logf is the hardware log2 (v_log_f32) times ln2 in extended precision (ln2 split
+    // into float hi + lo, one fma): bit-identical to torch on 1.2 M probed values, where a plain
+    // float multiply by ln2 differs in 3 % and this clang's __builtin_logf in 33 % of them
+    // (tools/torch_noise_probe.py, profiles/r5_torch_noise_probe.txt)
+    const float y = __builtin_amdgcn_logf(u);
+    const float ln = __builtin_fmaf(y, __builtin_bit_cast(float, 0x3f317218u), y * __builtin_bit_cast(float, 0xb102e308u));
+    const float lg = u >= 1.0f - 5.96046448e-08f ? -5.96046448e-08f : ln;
     return -1.0f * lg;
 }
 
