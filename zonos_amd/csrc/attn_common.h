@@ -88,9 +88,12 @@ ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int
 // keeping a whole slice in flight while it multiplies the previous one, and reads the pieces into
 // the same KVFrag registers (ds_read_b128 at the lane's 16 B: the image is the cache's own fragment
 // order). The attention-shaped stream probe reads 2-3 % faster this way than with register loads
-// (profiles/r3_attn_stream_probe.txt: dma16-nt vs base-nt). ZK_ATT_DMA = 0: register loads only.
+// (profiles/r3_attn_stream_probe.txt: dma16-nt vs base-nt), but inside the decode step the kernel
+// takes the same time either way (73.2 vs 73.1-73.4 us per launch at c3, same box, twice;
+// profiles/r5_attn_dma_ab.txt), so the product keeps the register form (ZK_ATT_DMA = 0; 1 selects
+// the DMA form, parity-green: 149 GPU tests).
 #ifndef ZK_ATT_DMA
-#define ZK_ATT_DMA 1
+#define ZK_ATT_DMA 0
 #endif
 constexpr int AT_RING = 16 * 1024;     // LDS ring bytes per wave
 // one 1 KB piece by LDS-DMA to the wave-uniform LDS byte address `lds`, non-temporal. Inline asm so
