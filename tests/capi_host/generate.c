@@ -9,12 +9,14 @@
  * Test helper of tests/test_gpu_capi_host.py (which writes the input file and checks the codes).
  *   usage: generate <input.bin> <output.bin>
  * Input (little endian): int32 header[16] = {magic 0x5a4b4831, D, n_layer, H, Hkv, d_ff, B, Lc, P,
- * max_new, head_rows, poll_every, rp_window, top_k, 0, 0}, float32 fparams[8] = {eps, cfg_scale,
- * temperature, top_p, min_p, linear, conf, quad}, float32 rep_penalty, uint64 seed, then bf16
+ * max_new, head_rows, poll_every, rp_window, top_k, noise_mode, noise_stride}, float32 fparams[8] = {eps,
+ * cfg_scale, temperature, top_p, min_p, linear, conf, quad}, float32 rep_penalty, uint64 seed (noise_mode 1:
+ * + uint64 noise_offset, uint64 noise_incr -- torch's GPU exponential_ stream, zk_gen_state), then bf16
  * tensors per layer (norm.w, norm.b, in_proj [3D'][D], out_proj [D][D], norm2.w, norm2.b,
  * fc1 [2F][D], fc2 [D][F]), norm_f.w, norm_f.b, 9 embeddings [1026][D], 9 heads [head_rows][D],
  * fp32 RoPE table [16384][hd/2][2], bf16 conditioning [2B][Lc][D], int64 prefix codes [B][9][P].
- * Output: int32 B, then per utterance int32 length T_i and int64 codes [9][T_i]. */
+ * Output: int32 B, then per utterance int32 length T_i and int64 codes [9][T_i]; stdout reports the
+ * sampler calls made (scal[2] + scal[4]: the Philox offset a torch-noise run consumed is calls * incr). */
 #include <hip/hip_runtime_api.h>
 #include <math.h>
 #include <stdint.h>
@@ -95,6 +97,11 @@ int main(int argc, char** argv) {
     rd(&rp, sizeof rp);
     rd(&seed, sizeof seed);
     if (hdr[0] != 0x5a4b4831) { fprintf(stderr, "generate: bad magic\n"); return 2; }
+    uint64_t noise_off = 0, noise_incr = 0;
+    if (hdr[14]) {
+        rd(&noise_off, sizeof noise_off);
+        rd(&noise_incr, sizeof noise_incr);
+    }
     const int D = hdr[1], NL = hdr[2], H = hdr[3], Hk = hdr[4], Fd = hdr[5], B = hdr[6], Lc = hdr[7], P = hdr[8];
     const int max_new = hdr[9], head_rows = hdr[10], poll_every = hdr[11];
     const int hd = D / H, Nqkv = (H + 2 * Hk) * hd, R = 2 * B;
@@ -191,6 +198,8 @@ int main(int argc, char** argv) {
     d.st.tok1 = (int32_t*)dzero((size_t)B * NCB * 4);
     d.st.delayed = (int64_t*)dalloc((size_t)B * NCB * Ld * 8);
     d.st.B = B; d.st.K = NCB; d.st.Ld = Ld; d.st.V = VOCAB; d.st.seed = seed; d.st.row_base = 0;
+    d.st.noise_mode = hdr[14]; d.st.noise_offset = noise_off; d.st.noise_stride = hdr[15];
+    d.st.noise_incr = (int32_t)noise_incr;
     d.sp.cfg_scale = fp[1]; d.sp.temperature = fp[2]; d.sp.top_p = fp[3]; d.sp.min_p = fp[4];
     d.sp.linear = fp[5]; d.sp.conf = fp[6]; d.sp.quad = fp[7]; d.sp.top_k = hdr[13]; d.sp.rp_window = hdr[12];
     d.sp.force_full_length = 0;
@@ -267,6 +276,6 @@ int main(int argc, char** argv) {
             }
     }
     fclose(fo);
-    printf("generate: B=%d, %d decode steps, offset %d\n", B, done_steps, offset);
+    printf("generate: B=%d, %d decode steps, offset %d, sampler calls %d\n", B, done_steps, offset, sc[2] + sc[4]);
     return 0;
 }

@@ -186,3 +186,31 @@ def test_generate_reference_noise_graph_equals_eager():
         offs.append(int(g.get_offset()))
     assert offs[0] == offs[1]
     assert all(torch.equal(x, y) for x, y in zip(*outs))
+
+
+def test_hybrid_reference_noise_graph_equals_eager():
+    """The hybrid engine (HybridDecoder shares generate()) with the reference's noise: graph replay ==
+    eager launches, codes and generator offset; the offset advanced by (prefill + steps + resamples)
+    calls of the [B][9][1026] policy increment."""
+    from oracle import hybrid_ref as HR
+
+    from .test_gpu_hybrid import TINYH
+    from .test_gpu_hybrid import _engine as hybrid_engine
+    from zonos_amd.sampling import torch_noise_policy
+    W = HR.make_weights(TINYH, seed=2, head_scale=4.0)
+    B, Lc, P, new = 3, 12, 4, 20
+    cond = zonos_ref.synthetic_conditioning(B, Lc, TINYH.d_model).to(DEV)
+    prefix = zonos_ref.synthetic_prefix_codes(B, P).to(DEV)
+    sp = dict(temperature=1.0, top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
+              repetition_penalty_window=8)
+    eng = hybrid_engine(W)
+    _, incr = torch_noise_policy(B * 9 * 1026, DEV)
+    outs, offs = [], []
+    for graph, poll in ((True, 6), (False, 1)):
+        g = torch.Generator(device=DEV)
+        g.manual_seed(77)
+        outs.append(eng.generate(cond, prefix, new, 2.0, B, sp, noise="torch", generator=g, use_graph=graph,
+                                 poll_every=poll))
+        offs.append(int(g.get_offset()))
+    assert offs[0] == offs[1] and offs[0] % incr == 0 and offs[0] // incr >= new, (offs, incr)
+    assert all(torch.equal(x, y) for x, y in zip(*outs))
