@@ -251,6 +251,10 @@ struct RowCtx {
 };
 
 // Everything after the logits are in registers: rep-penalty, shaping, race / argmax.
+// TN: the noise is torch's stream (c.noff, c.nstride, c.ebase), else the keyed one -- a template
+// argument, so neither sampler carries the other's branch (a runtime test cost 2-3 us per B = 1 step,
+// profiles/r5_torch_noise_branch_ab.txt)
+template <bool TN>
 ZK_DEV int sample_row(float* x, const RowCtx& c, const zk_sampling_params& sp, Smem& s) {
     const int V = c.V;
     // ---- repetition penalty (sampling.py:142-169); rp == 1 is an exact identity
@@ -309,12 +313,13 @@ ZK_DEV int sample_row(float* x, const RowCtx& c, const zk_sampling_params& sp, S
     for (int i = 0; i < NPT; ++i) {
         const int v = threadIdx.x + NT * i;
         if (v < V)
-            x[i] = __fdiv_rn(x[i], c.nstride > 0 ? torch_exp_noise(c.seed, c.noff, c.ebase + v, c.nstride)
-                                                 : exp_noise(c.seed, c.step, c.draw, c.row, c.k, v));
+            x[i] = __fdiv_rn(x[i], TN ? torch_exp_noise(c.seed, c.noff, c.ebase + v, c.nstride)
+                                      : exp_noise(c.seed, c.step, c.draw, c.row, c.k, v));
     }
     return block_argmax(x, V, s);
 }
 
+template <bool TN>
 __global__ __launch_bounds__(NT) void k_sample_logits(const float* logits, int B, int K, int V,
                                                       const int64_t* gen, int gen_stride, int gen_len,
                                                       const float* rp, zk_sampling_params sp, uint64_t seed,
@@ -331,11 +336,12 @@ __global__ __launch_bounds__(NT) void k_sample_logits(const float* logits, int B
     }
     RowCtx c{b, k, V, gen ? gen + ((size_t)b * K + k) * gen_stride : nullptr, gen_len,
              rp ? rp[b] : 1.f, step, draw, row_base + b, seed, noff, nstride, ((long)b * K + k) * V};
-    const int t = sample_row(x, c, sp, s);
+    const int t = sample_row<TN>(x, c, sp, s);
     if (threadIdx.x == 0) out[(size_t)b * K + k] = t;
 }
 
 // Engine sampler: CFG-combine the heads GEMM slabs, bias, EOS masks, sample.
+template <bool TN>
 __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nsplit, zk_gen_state st,
                                                      zk_sampling_params sp, int prefill, int draw,
                                                      float* dbg) {
@@ -424,7 +430,7 @@ __global__ __launch_bounds__(NT) void k_sample_heads(const float* part, int nspl
              prefill ? 1.f : rpb, prefill ? 0 : step, draw, st.row_base + b, st.seed,
              st.noise_offset + (uint64_t)call * (uint64_t)st.noise_incr, st.noise_mode ? st.noise_stride : 0,
              ((long)(st.row_base + b) * K + k) * V};
-    const int t = sample_row(x, c, sp, s);
+    const int t = sample_row<TN>(x, c, sp, s);
     if (threadIdx.x == 0) (draw ? st.tok1 : st.tok0)[b * K + k] = t;
 }
 
@@ -526,7 +532,7 @@ extern "C" int zk_sample_logits(const float* logits, int B, int K, int V, const 
     ZK_REQUIRE(B > 0 && K > 0, "zk_sample_logits: empty batch");
     ZK_REQUIRE(sp != nullptr, "zk_sample_logits: null params");
     ZK_REQUIRE(sp->top_k >= 0 && sp->rp_window >= 0, "zk_sample_logits: negative top_k/window");
-    hipLaunchKernelGGL(k_sample_logits, dim3(B * K), dim3(NT), 0, (hipStream_t)stream, logits, B, K, V,
+    hipLaunchKernelGGL(k_sample_logits<false>, dim3(B * K), dim3(NT), 0, (hipStream_t)stream, logits, B, K, V,
                        generated, gen_stride, gen_len, rp, *sp, seed, step, draw, row_base, (uint64_t)0, 0, out);
     ZK_CHECK_LAUNCH("zk_sample_logits");
     return 0;
@@ -540,7 +546,7 @@ extern "C" int zk_sample_logits_torch(const float* logits, int B, int K, int V, 
     ZK_REQUIRE(sp != nullptr, "zk_sample_logits_torch: null params");
     ZK_REQUIRE(sp->top_k >= 0 && sp->rp_window >= 0, "zk_sample_logits_torch: negative top_k/window");
     ZK_REQUIRE(stride > 0 && stride % 256 == 0, "zk_sample_logits_torch: stride %d (256 x grid)", stride);
-    hipLaunchKernelGGL(k_sample_logits, dim3(B * K), dim3(NT), 0, (hipStream_t)stream, logits, B, K, V,
+    hipLaunchKernelGGL(k_sample_logits<true>, dim3(B * K), dim3(NT), 0, (hipStream_t)stream, logits, B, K, V,
                        generated, gen_stride, gen_len, rp, *sp, seed, 0, 0, 0, offset, stride, out);
     ZK_CHECK_LAUNCH("zk_sample_logits_torch");
     return 0;
@@ -578,8 +584,11 @@ extern "C" int zk_sample_heads(const float* part, int nsplit, const zk_gen_state
                                void* stream) {
     ZK_REQUIRE(st && sp && part, "zk_sample_heads: null argument");
     ZK_REQUIRE(st->V > 0 && st->V <= NT * NPT, "zk_sample_heads: V=%d unsupported", st->V);
-    hipLaunchKernelGGL(k_sample_heads, dim3(st->B * st->K), dim3(NT), 0, (hipStream_t)stream, part, nsplit,
-                       *st, *sp, prefill, draw, dbg_logits);
+    ZK_REQUIRE(!st->noise_mode || (st->noise_stride > 0 && st->noise_stride % 256 == 0 && st->noise_incr > 0),
+               "zk_sample_heads: torch noise needs a stride (256 x grid) and an increment (zk_torch_noise_policy)");
+    auto kern = st->noise_mode ? k_sample_heads<true> : k_sample_heads<false>;
+    hipLaunchKernelGGL(kern, dim3(st->B * st->K), dim3(NT), 0, (hipStream_t)stream, part, nsplit, *st, *sp, prefill,
+                       draw, dbg_logits);
     ZK_CHECK_LAUNCH("zk_sample_heads");
     return 0;
 }
