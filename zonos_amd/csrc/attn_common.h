@@ -83,47 +83,6 @@ ZK_DEV void load_kv(KVFrag& f, const bf16_t* kb, const bf16_t* vb, int Smax, int
     for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld_kv<NT>(v0 + dt * 512);
 }
 
-// LDS-DMA form of the key loop (KVNT launches, the large-batch decode): every wave streams its K / V
-// slices through its own 16 KB LDS ring (16 x 1 KB pieces = one 32-key slice) by global_load_lds nt,
-// keeping a whole slice in flight while it multiplies the previous one, and reads the pieces into
-// the same KVFrag registers (ds_read_b128 at the lane's 16 B: the image is the cache's own fragment
-// order). The attention-shaped stream probe reads 2-3 % faster this way than with register loads
-// (profiles/r3_attn_stream_probe.txt: dma16-nt vs base-nt), but inside the decode step the kernel
-// takes the same time either way (73.2 vs 73.1-73.4 us per launch at c3, same box, twice;
-// profiles/r5_attn_dma_ab.txt), so the product keeps the register form (ZK_ATT_DMA = 0; 1 selects
-// the DMA form, parity-green: 149 GPU tests).
-#ifndef ZK_ATT_DMA
-#define ZK_ATT_DMA 0
-#endif
-constexpr int AT_RING = 16 * 1024;     // LDS ring bytes per wave
-// one 1 KB piece by LDS-DMA to the wave-uniform LDS byte address `lds`, non-temporal. Inline asm so
-// hipcc's waitcnt pass does not treat the pending LDS write as aliasing the ring's ds_reads (it
-// would wait vmcnt(0) before each); the key loop counts its own pieces.
-ZK_DEV void at_glds_nt(const void* gsrc, uint32_t lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds)
-                 : "memory");
-}
-// pieces [P0, P1) of the slice at key_base: K pieces 0-7 ([h][ks]), V pieces 8-15 ([dt])
-template <int P0, int P1>
-ZK_DEV void dma_kv(const bf16_t* kb, const bf16_t* vb, int key_base, int lane, uint32_t ring) {
-    const bf16_t* k0 = kb + (size_t)(key_base >> 5) * 4096 + lane * 8;
-    const bf16_t* v0 = vb + (size_t)(key_base >> 5) * 4096 + lane * 8;
-#pragma unroll
-    for (int i = P0; i < P1; ++i) at_glds_nt(i < 8 ? k0 + i * 512 : v0 + (i - 8) * 512, ring + i * 1024);
-}
-template <int P0, int P1>
-ZK_DEV void ring_read(KVFrag& f, const char* ring, int lane) {
-#pragma unroll
-    for (int i = P0; i < P1; ++i) {
-        const uint4 v = *reinterpret_cast<const uint4*>(ring + i * 1024 + lane * 16);
-        if (i < 8) f.k[i >> 2][i & 3] = v;
-        else f.v[i - 8] = v;
-    }
-}
-
 struct AttnState {
     float m, l;
     f32x4 o[8];      // o[dt][i] = O^T[d = dt*16 + 4lg + i][head = ln]
@@ -283,8 +242,7 @@ template <bool FUSED, bool NEOX, bool KVNT, bool COMB, class Bar, class Issued>
 ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, int split, int nsplit, int g, int r,
                            const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H, int Hkv, int Smax, int ctx,
                            float* work, float scale, bf16_t* out, const float* part, int gsplit, const float* freqs,
-                           uint32_t* cnt, char* ring_base = nullptr) {
-    constexpr bool DMA = ZK_ATT_DMA && KVNT;
+                           uint32_t* cnt) {
     constexpr int HD = 128;
     auto& s_m = sm.s_m;
     auto& s_l = sm.s_l;
@@ -322,19 +280,11 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
     // that of reading the cache. The first key block can therefore be fetched before the prologue.
     const int pos = ctx - 1;
     const bool early = FUSED && kbw > kb0;
-    const char* ring = ring_base + w * AT_RING;
-    const uint32_t ring_lds = DMA ? __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring) : 0u;
-    if constexpr (DMA) {     // the first slice is in flight during the prologue
-        if (kbw > kb0) dma_kv<0, 16>(kb, vb, kb0 * AT_KB + 32 * w, lane, ring_lds);
-    } else if (early) {      // the first TWO key blocks are in flight during the prologue
+    if (early) {      // the first TWO key blocks are in flight during the prologue
         load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         if (!ZK_ATT_TRIM || kb0 + 1 < kbw) load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
     }
     if (issued()) {          // skip: nothing is written (the loads above are in bounds)
-        if constexpr (DMA) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may outlive the workgroup
-            return;
-        }
         if (early) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -413,25 +363,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    if (DMA && kbw > kb0) {
-        // ring: slice `it` in flight (16 pieces, issued in order); read its K half once 8 pieces are
-        // left outstanding, re-issue those slots for slice it + 1, then the V half; multiply slice it
-        // while slice it + 1 streams in
-        for (int it = kb0; it < kbw; ++it) {
-            const bool nxt = it + 1 < kbw;
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            ring_read<0, 8>(fa, ring, lane);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (nxt) dma_kv<0, 8>(kb, vb, (it + 1) * AT_KB + 32 * w, lane, ring_lds);
-            if (nxt) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            ring_read<8, 16>(fa, ring, lane);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (nxt) dma_kv<8, 16>(kb, vb, (it + 1) * AT_KB + 32 * w, lane, ring_lds);
-            if (FUSED) patch_kv(fa, s_kn, s_vn, it * AT_KB + 32 * w, pos, ln, lg);
-            attn_step(st, fa, qf, it * AT_KB + 32 * w, ctx, scale, lg);
-        }
-    } else if (kbw > kb0) {
+    if (kbw > kb0) {
         if (!early) load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
         for (int it = kb0; it < kbw; it += 2) {
             if (!(early && it == kb0) && (!ZK_ATT_TRIM || it + 1 < kbw))
@@ -542,7 +474,6 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
                                                         const float* part, int gsplit, const float* freqs,
                                                         uint32_t* cnt = nullptr) {
     __shared__ AttnSmem sm;
-    extern __shared__ __attribute__((aligned(16))) char at_ring[];   // AT_RING per wave (DMA form)
     // both step scalars in one round trip; the skip word is tested once the first key blocks'
     // loads are in flight (issued -> return), so its latency overlaps theirs
     const int sk = ld_word(skip);
@@ -551,16 +482,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     const int ctx = min(ctx0 + uni(ld_word(ctx_dev)), Smax);
     attn_decode_wg<FUSED, NEOX, KVNT, COMB>(sm, [] { __syncthreads(); }, [sk] { return uni(sk) != 0; }, blockIdx.x,
                                            gridDim.x, blockIdx.y, blockIdx.z, q, kc, vt, R, H, Hkv, Smax, ctx, work,
-                                           scale, out, part, gsplit, freqs, cnt, at_ring);
-}
-
-// dynamic LDS of a k_attn_decode launch: the DMA form's rings (4 waves)
-template <bool KVNT>
-constexpr int at_dyn_lds() { return (ZK_ATT_DMA && KVNT) ? 4 * AT_RING : 0; }
-template <class K>
-inline void at_prepare(K kern, int lds) {
-    if (lds > 0)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                                           scale, out, part, gsplit, freqs, cnt);
 }
 
 }  // namespace

@@ -647,9 +647,7 @@ extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt
     const float scale = 1.0f / sqrtf((float)hd);
     const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
     auto kern = kvnt ? k_attn_decode<false, false, true> : k_attn_decode<false, false, false>;
-    const int lds = kvnt ? at_dyn_lds<true>() : 0;
-    at_prepare(kern, lds);
-    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), lds, (hipStream_t)stream,
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (bf16_t*)k_cache, (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work,
                        scale, (bf16_t*)out, skip, nullptr, 0, nullptr, nullptr);
     ZK_CHECK_LAUNCH("zk_attn_decode");
@@ -682,9 +680,7 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
     const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
     auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true> : k_attn_decode<true, true, false>)
                           : (kvnt ? k_attn_decode<true, false, true> : k_attn_decode<true, false, false>);
-    const int lds = kvnt ? at_dyn_lds<true>() : 0;
-    at_prepare(kern, lds);
-    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), lds, (hipStream_t)stream, dbgq, (bf16_t*)k_cache,
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq, (bf16_t*)k_cache,
                        (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out, skip, part,
                        gemm_nsplit, freqs, nullptr);
     ZK_CHECK_LAUNCH("zk_attn_decode_qkv");
@@ -712,9 +708,7 @@ extern "C" int zk_attn_decode_qkv_part(const float* part, int gemm_nsplit, const
     const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
     auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true> : k_attn_decode<true, true, false>)
                           : (kvnt ? k_attn_decode<true, false, true> : k_attn_decode<true, false, false>);
-    const int lds = kvnt ? at_dyn_lds<true>() : 0;
-    at_prepare(kern, lds);
-    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), lds, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
                        (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, nullptr, skip, part,
                        gemm_nsplit, freqs, nullptr);
     ZK_CHECK_LAUNCH("zk_attn_decode_qkv_part");
@@ -740,9 +734,7 @@ extern "C" int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const f
     const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
     auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true, true> : k_attn_decode<true, true, false, true>)
                           : (kvnt ? k_attn_decode<true, false, true, true> : k_attn_decode<true, false, false, true>);
-    const int lds = kvnt ? at_dyn_lds<true>() : 0;
-    at_prepare(kern, lds);
-    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), lds, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
                        (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out, skip, part,
                        gemm_nsplit, freqs, counters);
     ZK_CHECK_LAUNCH("zk_attn_decode_qkv_sc");
