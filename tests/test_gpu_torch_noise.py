@@ -53,14 +53,17 @@ def test_policy_matches_oracle_and_device():
                                                                  p.max_threads_per_multi_processor)
 
 
-def test_sample_from_logits_default_is_the_reference_stream():
+@pytest.mark.parametrize("B", [4, 64, 300])
+def test_sample_from_logits_default_is_the_reference_stream(B):
     """sample_from_logits without a seed races against exactly the noise torch's exponential_
     would give the reference on this generator state, and leaves the generator where that call
     leaves it; greedy calls draw nothing. Tokens = the oracle sampler (the reference's
     algorithm, pinned by sampler.npz) fed that noise; fp32 softmax/exp differ in the last ulp
-    between CPU and GPU, so at most 1 flipped token in all cases (as test_sampler_golden_exact)."""
+    between CPU and GPU, so at most 1 flipped token per 2,000 (test_sampler_golden_exact allows 1 in its
+    cases). B = 64: the c3 sampler call (torch's grid capped at 2048 blocks); B = 300: two iterations of
+    torch's grid-stride loop (an 8-offset call)."""
     from zonos_amd.sampling import sample_from_logits
-    B, K, V = 4, 9, 1026
+    K, V = 9, 1026
     gen = torch.Generator().manual_seed(5)
     logits = (torch.randn(B, K, V, generator=gen) * 3).to(DEV)
     hist = torch.randint(0, 1024, (B, K, 12), generator=gen).to(DEV)
@@ -80,7 +83,7 @@ def test_sample_from_logits_default_is_the_reference_stream():
         exp = zonos_ref.sample(logits.cpu(), q.cpu(), generated_tokens=hist.cpu(), repetition_penalty=2.5,
                                repetition_penalty_window=8, **sp).squeeze(-1)
         flips += int((tok != exp).sum())
-    assert flips <= 1, flips
+    assert flips <= max(1, 3 * B * K // 2000), flips
     torch.manual_seed(7)
     off0 = int(g.get_offset())
     sample_from_logits(logits, temperature=0.0)
