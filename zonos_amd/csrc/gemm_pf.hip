@@ -27,6 +27,17 @@ constexpr int PF_BM = 256, PF_BN = 256, PF_NT = 512;
 #ifndef ZK_PF_EPI
 #define ZK_PF_EPI 1                        // LDS-staged whole-row epilogues (0: direct register stores, A/B)
 #endif
+// diagnostic builds only (timing of the main loop's parts; results are wrong): NOWAIT skips the copy
+// waits (the barrier stays), NOMFMA the MFMAs (the LDS reads stay), NOLDS the LDS fragment reads
+#ifndef ZK_PF_DIAG_NOWAIT
+#define ZK_PF_DIAG_NOWAIT 0
+#endif
+#ifndef ZK_PF_DIAG_NOMFMA
+#define ZK_PF_DIAG_NOMFMA 0
+#endif
+#ifndef ZK_PF_DIAG_NOLDS
+#define ZK_PF_DIAG_NOLDS 0
+#endif
 
 // Activation rows in LDS: BKS-deep steps give rows of 2 * BKS bytes. The 16-B chunk c of row r is
 // stored at chunk c ^ swz(r), which makes every ds_read_b128 of an A fragment (16 rows x one chunk
@@ -245,7 +256,8 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
     for (int kt = 0; kt < nk; ++kt) {
         // step kt's copies: everything issued after them may stay in flight
         const int after = min(NSTG - 2, nk - 1 - kt);
-        if constexpr (NSTG >= 4) {
+        if constexpr (ZK_PF_DIAG_NOWAIT) {
+        } else if constexpr (NSTG >= 4) {
             if (after >= 2) pf_vm_wait<2 * LPS>();
             else if (after == 1) pf_vm_wait<LPS>();
             else pf_vm_wait<0>();
@@ -268,14 +280,21 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
             uint4 bf[4];
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
-                bf[nt] = *reinterpret_cast<const uint4*>(sb + (((wc * 4 + nt) * KSS + ks) << 10) + lane * 16);
+                bf[nt] = ZK_PF_DIAG_NOLDS ? make_uint4(lane, nt, ks, kt)
+                                          : *reinterpret_cast<const uint4*>(sb + (((wc * 4 + nt) * KSS + ks) << 10) + lane * 16);
 #pragma unroll
             for (int mt = 0; mt < 8; ++mt) {
-                const uint4 a = *reinterpret_cast<const uint4*>(sa + pf_a_off<BKS>(wr * 128 + mt * 16 + ln, ks * 4 + lg));
+                const uint4 a = ZK_PF_DIAG_NOLDS ? make_uint4(mt, lane, ks, kt)
+                                                 : *reinterpret_cast<const uint4*>(sa + pf_a_off<BKS>(wr * 128 + mt * 16 + ln, ks * 4 + lg));
 #pragma unroll
-                for (int nt = 0; nt < 4; ++nt)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(bf[nt]), acc[mt][nt], 0,
-                                                                          0, 0);
+                for (int nt = 0; nt < 4; ++nt) {
+                    if constexpr (ZK_PF_DIAG_NOMFMA) {
+                        acc[mt][nt][0] += __uint_as_float(a.x ^ bf[nt].y);
+                    } else {
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(bf[nt]), acc[mt][nt], 0,
+                                                                              0, 0);
+                    }
+                }
             }
         }
     }
