@@ -123,12 +123,13 @@ def test_gemm_narrow_wide_workgroups_bit_identical(N, N2, nsplit):
     assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("M,N,K", [(16400, 4096, 1024), (8300, 2112, 512)])
+@pytest.mark.parametrize("M,N,K", [(16400, 4096, 1024), (8300, 2112, 512), (9000, 8256, 512)])
 def test_prefill_gemm_epilogues_consistent(M, N, K):
     """k_gemm_pf's LDS-staged epilogues (whole-row stores, round 5): the SwiGLU output of mode 1 is
     the SwiGLU of mode 0's fp32 output over the same interleaved weights (both modes accumulate in one
     K order), computed here with torch: equal except where expf and torch.exp round the silu
-    differently (<= 1 bf16 ulp of the product on a few elements); mode 0 against an fp32 reference."""
+    differently (<= 1 bf16 ulp of the product on a few elements); mode 0 against an fp32 reference.
+    N = 8256: mode 1 on 256 x 384 tiles (N >= 8192, partial last column tile), mode 0 on 256 x 256."""
     from zonos_amd._lib import call, ptr, stream_ptr
     from zonos_amd.engine import pack_weights
     g = torch.Generator(device="cpu").manual_seed(M)

@@ -9,8 +9,9 @@
 // XOR-swizzled 128-B row layout of the decode GEMM (lds_off: conflict-free ds_read_b128), the
 // weights as the fragment-packed image itself ([N/16][K/32][64 lanes][8]: every 16 x 32 B
 // fragment is a lane-linear 1 KB block, so the copy needs no address math and the read no swizzle).
-// The next step's stage is issued right after the barrier that retires the stage it overwrites,
-// so a whole step of MFMAs (64 per wave) covers its latency. Tiles are handed to the 8 XCDs in
+// The next step's stage is issued after the barrier that retires the stage it overwrites, one
+// piece per 4 MFMAs over the step's first k-slice (ZK_PF_SPREAD), so the rest of the step covers its
+// latency and the issues do not stall the MFMAs. Tiles are handed to the 8 XCDs in
 // contiguous runs and walked in 4 x 8 (row x column) blocks, so each XCD's L2 re-serves both
 // operands to the 32 workgroups it runs at once.
 //
@@ -23,7 +24,7 @@
 
 namespace {
 
-constexpr int PF_BM = 256, PF_BN = 256, PF_NT = 512;
+constexpr int PF_BM = 256, PF_NT = 512;
 #ifndef ZK_PF_EPI
 #define ZK_PF_EPI 1                        // LDS-staged whole-row epilogues (0: direct register stores, A/B)
 #endif
@@ -34,6 +35,14 @@ constexpr int PF_BM = 256, PF_BN = 256, PF_NT = 512;
 #endif
 #ifndef ZK_PF_DIAG_NOMFMA
 #define ZK_PF_DIAG_NOMFMA 0
+#endif
+// the refill of the next stage: piece j of a wave issued right after MFMA j * ZK_PF_SPREAD of the step
+// (0: all pieces at the top of the step). A burst of 8 LDS-DMA issues holds the wave's MFMAs back;
+// one piece per 4 MFMAs (over the step's first k-slice) measured fastest: fc1 3.31-3.38 -> 3.18 ms,
+// qkv 0.77 -> 0.73, o 0.47-0.48 -> 0.45, fc2 1.50 -> 1.42 (1, 2 or 8 MFMAs per piece, 32-deep stages
+// and 256 x 384 tiles slower; profiles/r5_prefill_spread_ab.txt)
+#ifndef ZK_PF_SPREAD
+#define ZK_PF_SPREAD 4
 #endif
 #ifndef ZK_PF_DIAG_NOLDS
 #define ZK_PF_DIAG_NOLDS 0
@@ -82,13 +91,13 @@ ZK_DEV void pf_tile(int L, int nwg, int tm, int tn, int& bm, int& bn) {
     (void)gcols;
 }
 
-// acc[mt][nt][i] = C[m0 + wr*128 + mt*16 + lg*4 + i][n0 + wc*64 + nt*16 + ln]
-template <int MODE>
-ZK_DEV void pf_epilogue(const f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc, int ln, int lg, int M, int N,
+// acc[mt][nt][i] = C[m0 + wr*128 + mt*16 + lg*4 + i][n0 + wc*16*NTN + nt*16 + ln]
+template <int MODE, int NTN>
+ZK_DEV void pf_epilogue(const f32x4 (&acc)[8][NTN], int m0, int n0, int wr, int wc, int ln, int lg, int M, int N,
                         float* __restrict__ C, bf16_t* __restrict__ Cb) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const int c0 = n0 + wc * 64 + nt * 16;
+    for (int nt = 0; nt < NTN; ++nt) {
+        const int c0 = n0 + wc * 16 * NTN + nt * 16;
         if (MODE == 0) {
             const int n = c0 + ln;
             if (n < N) {
@@ -122,51 +131,64 @@ ZK_DEV void pf_epilogue(const f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc
 // Epilogues staged through the (then idle) LDS stages, so every global store writes whole rows:
 // the register layout above writes 16 columns of 4 rows per instruction (64-B fp32 pieces, or 16-B
 // bf16 pieces from half the lanes in the SwiGLU form).
-//   mode 1: the bf16-rounded y / gate columns of the whole 256 x 256 tile (row stride PF_ES halves,
-//           padded against bank conflicts), then every lane computes y * silu(gate) for 8 outputs
-//           and stores them as one 16-B piece: 16 lanes write a 256-B row segment (the arithmetic and
-//           rounding points of pf_epilogue<1>, bit-identical);
-//   mode 0: the fp32 tile in two halves of 128 rows (row stride PF_EF floats), each stored as whole
-//           1 KB rows (one wave instruction per row).
-constexpr int PF_ES = PF_BN + 8;                   // mode 1 staging row stride (halves)
-constexpr int PF_EF = PF_BN + 4;                   // mode 0 staging row stride (floats)
-constexpr int PF_EPI_LDS1 = PF_BM * PF_ES * 2;     // 135,168 B
-constexpr int PF_EPI_LDS0 = (PF_BM / 2) * PF_EF * 4;   // 133,120 B
-template <int MODE>
-ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][4], char* smem, int m0, int n0, int wr, int wc, int ln, int lg,
+//   mode 1: the bf16-rounded y / gate columns of the tile (row stride pf_es halves, padded against
+//           bank conflicts; the 256 x 384 tile in two passes of 128 rows, one per wave row half),
+//           then every lane computes y * silu(gate) for 8 outputs and stores them as one 16-B piece:
+//           a row's 16-column groups write one contiguous row segment (the arithmetic and rounding
+//           points of pf_epilogue<1>, bit-identical);
+//   mode 0: the fp32 tile in two halves of 128 rows (row stride pf_ef floats), each stored as whole
+//           1 KB rows (one wave instruction per row; 256-column tiles only).
+template <int NTN> constexpr int pf_bn = 64 * NTN;                 // tile columns: 4 waves x NTN x 16
+template <int NTN> constexpr int pf_es = pf_bn<NTN> + 8;          // mode 1 staging row stride (halves)
+template <int NTN> constexpr int pf_rh = NTN > 4 ? 128 : 256;     // mode 1 rows per staging pass
+template <int NTN> constexpr int pf_ef = pf_bn<NTN> + 4;          // mode 0 staging row stride (floats)
+template <int NTN> constexpr int pf_epi_lds1 = pf_rh<NTN> * pf_es<NTN> * 2;   // 135,168 B (4) / 100,352 B (6)
+template <int NTN> constexpr int pf_epi_lds0 = NTN == 4 ? (PF_BM / 2) * pf_ef<NTN> * 4 : 0;   // 133,120 B
+template <int MODE, int NTN>
+ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][NTN], char* smem, int m0, int n0, int wr, int wc, int ln, int lg,
                             int M, int N, float* __restrict__ C, bf16_t* __restrict__ Cb) {
+    static_assert(MODE == 1 || NTN == 4, "fp32 staged epilogue: 256-column tiles");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();                                   // every wave's last stage read
     if constexpr (MODE == 1) {
+        constexpr int ES = pf_es<NTN>, RH = pf_rh<NTN>, G = pf_bn<NTN> / 16;   // G 16-column groups per row
         bf16_t* t = reinterpret_cast<bf16_t*>(smem);
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    t[(wr * 128 + mt * 16 + lg * 4 + i) * PF_ES + wc * 64 + nt * 16 + ln] = f2bf(acc[mt][nt][i]);
-        __syncthreads();
         const int F = N / 2, f0 = n0 / 2;
-        const int gi = tid & 15;                       // 16-column group of the row: outputs f0 + 8 gi ..
 #pragma unroll
-        for (int it = 0; it < PF_BM / 32; ++it) {
-            const int r = it * 32 + (tid >> 4), m = m0 + r;
-            if (m >= M || f0 + gi * 8 >= F) continue;
-            const bf16_t* src = t + r * PF_ES + gi * 16;
-            const uint4 yv = *reinterpret_cast<const uint4*>(src), gv = *reinterpret_cast<const uint4*>(src + 8);
-            float y[8], g[8], o[8];
-            unpack8(yv, y);
-            unpack8(gv, g);
+        for (int pass = 0; pass < PF_BM / RH; ++pass) {
+            if (RH == PF_BM || wr == pass) {
+                const int rb = RH == PF_BM ? wr * 128 : 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float sl = round_bf(g[j] / (1.0f + expf(-g[j])));     // F.silu in bf16
-                o[j] = y[j] * sl;
+                for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+                    for (int nt = 0; nt < NTN; ++nt)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            t[(rb + mt * 16 + lg * 4 + i) * ES + wc * 16 * NTN + nt * 16 + ln] = f2bf(acc[mt][nt][i]);
             }
-            *reinterpret_cast<uint4*>(Cb + (size_t)m * F + f0 + gi * 8) = pack8(o);
+            __syncthreads();
+            // item q = (row q / G, group q % G): outputs f0 + 8 (q % G) .. + 7 of that row
+#pragma unroll 2
+            for (int q = tid; q < RH * G; q += PF_NT) {
+                const int r = q / G, gi = q - r * G, m = m0 + pass * RH + r;
+                if (m >= M || f0 + gi * 8 >= F) continue;
+                const bf16_t* src = t + r * ES + gi * 16;
+                const uint4 yv = *reinterpret_cast<const uint4*>(src), gv = *reinterpret_cast<const uint4*>(src + 8);
+                float y[8], g[8], o[8];
+                unpack8(yv, y);
+                unpack8(gv, g);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float sl = round_bf(g[j] / (1.0f + expf(-g[j])));     // F.silu in bf16
+                    o[j] = y[j] * sl;
+                }
+                *reinterpret_cast<uint4*>(Cb + (size_t)m * F + f0 + gi * 8) = pack8(o);
+            }
+            if (pass + 1 < PF_BM / RH) __syncthreads();   // the next pass overwrites the staging rows
         }
     } else {
+        constexpr int EF = pf_ef<NTN>;
         float* t = reinterpret_cast<float*>(smem);
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
@@ -174,10 +196,10 @@ ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][4], char* smem, int m0, int n0
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < 4; ++nt)
+                    for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            t[(mt * 16 + lg * 4 + i) * PF_EF + wc * 64 + nt * 16 + ln] = acc[mt][nt][i];
+                            t[(mt * 16 + lg * 4 + i) * EF + wc * 64 + nt * 16 + ln] = acc[mt][nt][i];
             }
             __syncthreads();
             // 128 rows x 1 KB: wave w stores rows w, w + 8, ...; lane L the floats 4L .. 4L + 3
@@ -185,7 +207,7 @@ ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][4], char* smem, int m0, int n0
             for (int r = w; r < 128; r += 8) {
                 const int m = m0 + half * 128 + r;
                 if (m < M && n0 + 4 * lane < N) {
-                    const f32x4 v = *reinterpret_cast<const f32x4*>(t + r * PF_EF + 4 * lane);
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(t + r * EF + 4 * lane);
                     *reinterpret_cast<f32x4*>(C + (size_t)m * N + n0 + 4 * lane) = v;
                 }
             }
@@ -194,23 +216,26 @@ ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][4], char* smem, int m0, int n0
     }
 }
 
-// BKS: K depth of one LDS stage (32 or 64); NSTG: stages in the ring (NSTG - 1 in flight).
-template <int MODE, int BKS, int NSTG>
+// BKS: K depth of one LDS stage (32 or 64); NSTG: stages in the ring (NSTG - 1 in flight);
+// NTN: 16-column tiles per wave (4: 256 x 256 workgroup tiles; 6: 256 x 384, 1.2x fewer fill bytes
+// per FLOP -- two 80 KB stages fill the 160 KB LDS).
+template <int MODE, int BKS, int NSTG, int NTN>
 __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__ A, long lda,
                                                       const bf16_t* __restrict__ W, int M, int N, int K,
                                                       float* __restrict__ C, bf16_t* __restrict__ Cb,
                                                       const int32_t* skip) {
     constexpr int KSS = BKS / 32;                        // 32-deep MFMA k-slices per stage
-    constexpr int AST = PF_BM * BKS * 2, BST = PF_BN * BKS * 2, ST = AST + BST;
+    constexpr int BN = pf_bn<NTN>;
+    constexpr int AST = PF_BM * BKS * 2, BST = BN * BKS * 2, ST = AST + BST;
     constexpr int RPP = 1024 / (2 * BKS);                // activation rows per 1 KB LDS-DMA piece
     constexpr int CPR = 2 * BKS / 16;                    // 16-B chunks per activation row
     constexpr int NA = AST / 1024 / 8, NB = BST / 1024 / 8;     // pieces per wave and stage
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (skip && *skip) return;
-    const int tm = (M + PF_BM - 1) / PF_BM, tn = (N + PF_BN - 1) / PF_BN;
+    const int tm = (M + PF_BM - 1) / PF_BM, tn = (N + BN - 1) / BN;
     int bm, bn;
     pf_tile(blockIdx.x, gridDim.x, tm, tn, bm, bn);
-    const int m0 = bm * PF_BM, n0 = bn * PF_BN;
+    const int m0 = bm * PF_BM, n0 = bn * BN;
     const int nk = K / BKS;
     const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ln = lane & 15, lg = lane >> 4;
@@ -243,12 +268,23 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
         for (int i = 0; i < NB; ++i) pf_glds(bsrc[i] + (size_t)kt * KSS * 512, sb + i * 8192);
     };
     constexpr int LPS = NA + NB;                         // LDS-DMA loads per wave and stage
+    // one piece j of the stage: activation pieces first, then weight pieces
+    auto issue_piece = [&](int kt, int st, int j) {
+        const uint32_t sa = lds0 + st * ST, sb = sa + AST;
+        if (j < NA) pf_glds(asrc[j] + kt * BKS, sa + j * 8192);
+        else pf_glds(bsrc[j - NA] + (size_t)kt * KSS * 512, sb + (j - NA) * 8192);
+    };
+    // ZK_PF_SPREAD = P > 0: the refill's pieces are issued between the step's MFMAs, piece j right after
+    // MFMA j * P of the step, instead of all at the top of the step (0)
+    constexpr int QS = KSS * 8;                          // MFMA groups (ks, mt) per step
+    constexpr int SP = ZK_PF_SPREAD;
+    static_assert(SP == 0 || (LPS - 1) * SP < QS * NTN, "spread: every piece inside the step");
 
-    f32x4 acc[8][4];
+    f32x4 acc[8][NTN];
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int nt = 0; nt < NTN; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
     for (int s0 = 0; s0 < NSTG - 1; ++s0)
@@ -272,43 +308,65 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt + NSTG - 1 < nk) issue(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
+        if (!ZK_PF_SPREAD && kt + NSTG - 1 < nk) issue(kt + NSTG - 1, (kt + NSTG - 1) % NSTG);
         const char* sa = smem + (kt % NSTG) * ST;
         const char* sb = sa + AST;
+        auto rd_a = [&](int q) -> uint4 {
+            const int ks = q >> 3, mt = q & 7;
+            return ZK_PF_DIAG_NOLDS ? make_uint4(mt, lane, ks, kt)
+                                    : *reinterpret_cast<const uint4*>(sa + pf_a_off<BKS>(wr * 128 + mt * 16 + ln, ks * 4 + lg));
+        };
+        auto rd_b = [&](int ks, int nt) -> uint4 {
+            return ZK_PF_DIAG_NOLDS ? make_uint4(lane, nt, ks, kt)
+                                    : *reinterpret_cast<const uint4*>(sb + (((wc * NTN + nt) * KSS + ks) << 10) + lane * 16);
+        };
+        uint4 bf[2][NTN];
 #pragma unroll
-        for (int ks = 0; ks < KSS; ++ks) {
-            uint4 bf[4];
+        for (int nt = 0; nt < NTN; ++nt) bf[0][nt] = rd_b(0, nt);
+        uint4 a = rd_a(0);
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-                bf[nt] = ZK_PF_DIAG_NOLDS ? make_uint4(lane, nt, ks, kt)
-                                          : *reinterpret_cast<const uint4*>(sb + (((wc * 4 + nt) * KSS + ks) << 10) + lane * 16);
+        for (int q = 0; q < QS; ++q) {
+            const int ks = q >> 3, mt = q & 7;
+            if (mt == 0 && ks > 0) {
 #pragma unroll
-            for (int mt = 0; mt < 8; ++mt) {
-                const uint4 a = ZK_PF_DIAG_NOLDS ? make_uint4(mt, lane, ks, kt)
-                                                 : *reinterpret_cast<const uint4*>(sa + pf_a_off<BKS>(wr * 128 + mt * 16 + ln, ks * 4 + lg));
+                for (int nt = 0; nt < NTN; ++nt) bf[ks & 1][nt] = rd_b(ks, nt);
+            }
 #pragma unroll
-                for (int nt = 0; nt < 4; ++nt) {
-                    if constexpr (ZK_PF_DIAG_NOMFMA) {
-                        acc[mt][nt][0] += __uint_as_float(a.x ^ bf[nt].y);
-                    } else {
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(bf[nt]), acc[mt][nt], 0,
-                                                                              0, 0);
-                    }
+            for (int nt = 0; nt < NTN; ++nt) {
+                if constexpr (ZK_PF_DIAG_NOMFMA) {
+                    acc[mt][nt][0] += __uint_as_float(a.x ^ bf[ks & 1][nt].y);
+                } else {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(bf[ks & 1][nt]), acc[mt][nt],
+                                                                          0, 0, 0);
+                }
+                if constexpr (SP != 0) {
+                    // no branch around the pieces (one basic block per step, so the LDS reads can be
+                    // scheduled ahead of the MFMAs): past the last step the refill re-reads step nk - 1
+                    // into the stage nothing reads any more (the epilogue drains vmcnt first)
+                    const int f = q * NTN + nt;
+                    if (f % SP == 0 && f / SP < LPS)
+                        issue_piece(min(kt + NSTG - 1, nk - 1), (kt + NSTG - 1) % NSTG, f / SP);
                 }
             }
+            if (q + 1 < QS) a = rd_a(q + 1);
         }
     }
 
-    if (ZK_PF_EPI && (MODE == 1 || N % 4 == 0)) pf_epilogue_lds<MODE>(acc, smem, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
-    else pf_epilogue<MODE>(acc, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
+    if constexpr (ZK_PF_EPI && (MODE == 1 || NTN == 4)) {
+        if (MODE == 1 || N % 4 == 0) {
+            pf_epilogue_lds<MODE, NTN>(acc, smem, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
+            return;
+        }
+    }
+    pf_epilogue<MODE, NTN>(acc, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
 }
 
 }  // namespace
 
-// The prefill regime of zk_gemm_bf16 (split 1, large M): true when the 256 x 256 kernel takes the call.
+// The prefill regime of zk_gemm_bf16 (split 1, large M): true when the 256-row-tile kernel takes the call.
 bool zk_gemm_pf_applies(int M, int N, int K, int nsplit) {
     if (nsplit != 1 || K % 64 != 0 || N % 64 != 0) return false;
-    const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + PF_BN - 1) / PF_BN);
+    const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + 255) / 256);
     return tiles >= 256;                              // at least one tile per CU
 }
 
@@ -318,21 +376,46 @@ bool zk_gemm_pf_applies(int M, int N, int K, int nsplit) {
 #ifndef ZK_PF_BKS
 #define ZK_PF_BKS 64
 #endif
+// 256 x 384 tiles for the SwiGLU (fc1) form when N >= 8192 (the partial last column tile wastes <= 1.6 %
+// of its MFMAs there); 0: 256 x 256 everywhere
+#ifndef ZK_PF_WIDE
+#define ZK_PF_WIDE 0
+#endif
 constexpr int PF_BKS = ZK_PF_BKS, PF_NSTG = PF_BKS == 64 ? 2 : 4;
-constexpr int PF_LDS_MAIN = PF_NSTG * (PF_BM + PF_BN) * PF_BKS * 2;
 constexpr int pf_max(int a, int b) { return a > b ? a : b; }
-constexpr int PF_LDS = pf_max(PF_LDS_MAIN, ZK_PF_EPI ? pf_max(PF_EPI_LDS1, PF_EPI_LDS0) : 0);
+template <int MODE, int NTN>
+constexpr int pf_lds() {
+    return pf_max(PF_NSTG * (PF_BM + pf_bn<NTN>) * PF_BKS * 2,
+                  ZK_PF_EPI ? (MODE == 1 ? pf_epi_lds1<NTN> : pf_epi_lds0<NTN>) : 0);
+}
+static_assert(pf_lds<1, 6>() <= 163840 && pf_lds<0, 4>() <= 163840 && pf_lds<1, 4>() <= 163840, "LDS");
+
+template <int MODE, int NTN>
+static int pf_launch(const void* A, long lda, const void* W, int M, int N, int K, float* C, void* Cb,
+                      const int32_t* skip, hipStream_t stream) {
+    const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + pf_bn<NTN> - 1) / pf_bn<NTN>);
+    ZK_REQUIRE(tiles < (1L << 31), "zk_gemm_bf16 (prefill): too many tiles");
+    auto kern = &k_gemm_pf<MODE, PF_BKS, PF_NSTG, NTN>;
+    constexpr int lds = pf_lds<MODE, NTN>();
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(PF_NT), lds, stream, (const bf16_t*)A, lda, (const bf16_t*)W,
+                       M, N, K, C, (bf16_t*)Cb, skip);
+    return 0;
+}
 
 int zk_gemm_pf(const void* A, long lda, const void* W, int M, int N, int K, int mode, float* C, void* Cb,
                const int32_t* skip, void* stream) {
-    const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + PF_BN - 1) / PF_BN);
-    ZK_REQUIRE(tiles < (1L << 31), "zk_gemm_bf16 (prefill): too many tiles");
     // (a staggered four-phase form of the step -- two wave groups offset by one barrier, reads of one
     // overlapping the other's MFMAs -- measured 1-3 % slower: DESIGN.md §6 round 4)
-    auto kern = mode == 0 ? &k_gemm_pf<0, PF_BKS, PF_NSTG> : &k_gemm_pf<1, PF_BKS, PF_NSTG>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, PF_LDS);
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(PF_NT), PF_LDS, (hipStream_t)stream, (const bf16_t*)A, lda,
-                       (const bf16_t*)W, M, N, K, C, (bf16_t*)Cb, skip);
+    const hipStream_t st = (hipStream_t)stream;
+    int rc;
+#if ZK_PF_WIDE
+    if (mode == 1 && N >= 8192) rc = pf_launch<1, 6>(A, lda, W, M, N, K, C, Cb, skip, st);
+    else
+#endif
+    if (mode == 0) rc = pf_launch<0, 4>(A, lda, W, M, N, K, C, Cb, skip, st);
+    else rc = pf_launch<1, 4>(A, lda, W, M, N, K, C, Cb, skip, st);
+    if (rc) return rc;
     ZK_CHECK_LAUNCH("zk_gemm_bf16 (prefill)");
     return 0;
 }
