@@ -71,6 +71,15 @@ ZK_DEV void pf_glds(const void* gsrc, uint32_t lds) {
                  : "v"(gsrc), "s"(lds)
                  : "memory");
 }
+// The same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset: one VGPR per
+// piece instead of a 64-bit address pair.
+ZK_DEV void pf_glds_s(const void* sbase, uint32_t voff, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds)
+                 : "memory");
+}
 
 // Tile order: workgroup id -> (row block, column block). Ids are dispatched round-robin over the
 // XCDs (id % 8); each XCD gets a contiguous run of the tile sequence (bijective for any count),
@@ -169,10 +178,9 @@ ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][NTN], char* smem, int m0, int 
             }
             __syncthreads();
             // item q = (row q / G, group q % G): outputs f0 + 8 (q % G) .. + 7 of that row
-#pragma unroll 2
-            for (int q = tid; q < RH * G; q += PF_NT) {
+            auto item = [&](int q) {
                 const int r = q / G, gi = q - r * G, m = m0 + pass * RH + r;
-                if (m >= M || f0 + gi * 8 >= F) continue;
+                if (m >= M || f0 + gi * 8 >= F) return;
                 const bf16_t* src = t + r * ES + gi * 16;
                 const uint4 yv = *reinterpret_cast<const uint4*>(src), gv = *reinterpret_cast<const uint4*>(src + 8);
                 float y[8], g[8], o[8];
@@ -184,6 +192,13 @@ ZK_DEV void pf_epilogue_lds(const f32x4 (&acc)[8][NTN], char* smem, int m0, int 
                     o[j] = y[j] * sl;
                 }
                 *reinterpret_cast<uint4*>(Cb + (size_t)m * F + f0 + gi * 8) = pack8(o);
+            };
+            if constexpr (NTN > 4) {                   // (the other row half's 192 accumulators are live)
+#pragma unroll 1
+                for (int q = tid; q < RH * G; q += PF_NT) item(q);
+            } else {
+#pragma unroll 2
+                for (int q = tid; q < RH * G; q += PF_NT) item(q);
             }
             if (pass + 1 < PF_BM / RH) __syncthreads();   // the next pass overwrites the staging rows
         }
@@ -243,36 +258,39 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
 
     // ---- loader addresses. Activation piece p = i * 8 + w covers tile rows RPP p .. RPP p + RPP - 1:
     // lane L lands at row RPP p + L / CPR, chunk slot L % CPR, which holds source chunk slot ^ swz(row)
-    const bf16_t* asrc[NA];
+    // (32-bit byte offsets from wave-uniform bases: the tile's first activation row and the packed
+    // weights; the packed image of one projection is < 4 GB, the activation offsets < 256 rows)
+    uint32_t aoff[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
         const int p = i * 8 + w, row = RPP * p + lane / CPR;
         const int m = min(m0 + row, M - 1);            // rows >= M compute garbage that is never stored
-        asrc[i] = A + (size_t)m * lda + (((lane % CPR) ^ pf_swz<BKS>(row)) << 3);
+        aoff[i] = (uint32_t)(((long)(m - m0) * lda + (((lane % CPR) ^ pf_swz<BKS>(row)) << 3)) * 2);
     }
+    const bf16_t* const abase = A + (size_t)m0 * lda;
     // weight block b = i * 8 + w: 16-column group b / KSS, k-slice b % KSS of the stage
-    const bf16_t* bsrc[NB];
+    uint32_t boff[NB];
     const int ntl = (N + 15) / 16;                      // packed 16-row tiles present (padded to 64 rows)
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
         const int b = i * 8 + w, g = n0 / 16 + b / KSS;
         const int gg = g < ntl ? g : 0;                 // groups past N stream group 0 (never stored)
-        bsrc[i] = W + ((size_t)gg * (K >> 5) + (b % KSS)) * 512 + lane * 8;
+        boff[i] = (uint32_t)((((long)gg * (K >> 5) + (b % KSS)) * 512 + lane * 8) * 2);
     }
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + w * 1024);
     auto issue = [&](int kt, int st) {
         const uint32_t sa = lds0 + st * ST, sb = sa + AST;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) pf_glds(asrc[i] + kt * BKS, sa + i * 8192);
+        for (int i = 0; i < NA; ++i) pf_glds_s(abase + kt * BKS, aoff[i], sa + i * 8192);
 #pragma unroll
-        for (int i = 0; i < NB; ++i) pf_glds(bsrc[i] + (size_t)kt * KSS * 512, sb + i * 8192);
+        for (int i = 0; i < NB; ++i) pf_glds_s(W + (size_t)kt * KSS * 512, boff[i], sb + i * 8192);
     };
     constexpr int LPS = NA + NB;                         // LDS-DMA loads per wave and stage
     // one piece j of the stage: activation pieces first, then weight pieces
     auto issue_piece = [&](int kt, int st, int j) {
         const uint32_t sa = lds0 + st * ST, sb = sa + AST;
-        if (j < NA) pf_glds(asrc[j] + kt * BKS, sa + j * 8192);
-        else pf_glds(bsrc[j - NA] + (size_t)kt * KSS * 512, sb + (j - NA) * 8192);
+        if (j < NA) pf_glds_s(abase + kt * BKS, aoff[j], sa + j * 8192);
+        else pf_glds_s(W + (size_t)kt * KSS * 512, boff[j - NA], sb + (j - NA) * 8192);
     };
     // ZK_PF_SPREAD = P > 0: the refill's pieces are issued between the step's MFMAs, piece j right after
     // MFMA j * P of the step, instead of all at the top of the step (0)
