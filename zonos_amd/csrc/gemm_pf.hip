@@ -33,6 +33,12 @@ constexpr int PF_BM = 256, PF_NT = 512;
 #ifndef ZK_PF_DIAG_NOWAIT
 #define ZK_PF_DIAG_NOWAIT 0
 #endif
+#ifndef ZK_PF_DIAG_NOFILL          // (no LDS-DMA at all: MFMAs + LDS reads + barriers only)
+#define ZK_PF_DIAG_NOFILL 0
+#endif
+#ifndef ZK_PF_DIAG_NOEPI           // (no epilogue stores)
+#define ZK_PF_DIAG_NOEPI 0
+#endif
 #ifndef ZK_PF_DIAG_NOMFMA
 #define ZK_PF_DIAG_NOMFMA 0
 #endif
@@ -59,6 +65,21 @@ ZK_DEV int pf_a_off(int r, int c) { return r * (2 * BKS) + ((c ^ pf_swz<BKS>(r))
 
 template <int N_>
 ZK_DEV void pf_vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory"); }
+// wait until at most `after` stages of LPS pieces are outstanding (after <= MAXA)
+template <int LPS, int MAXA>
+ZK_DEV void pf_wait_after(int after) {
+    static_assert(MAXA <= 3 && MAXA * LPS <= 63, "vmcnt field");
+    if constexpr (MAXA >= 3) {
+        if (after >= 3) { pf_vm_wait<3 * LPS>(); return; }
+    }
+    if constexpr (MAXA >= 2) {
+        if (after == 2) { pf_vm_wait<2 * LPS>(); return; }
+    }
+    if constexpr (MAXA >= 1) {
+        if (after == 1) { pf_vm_wait<LPS>(); return; }
+    }
+    pf_vm_wait<0>();
+}
 
 // LDS-DMA of one 1 KB piece (64 lanes x 16 B) to the wave-uniform LDS byte address `lds`. Inline asm:
 // hipcc's waitcnt pass would otherwise treat the pending LDS write as aliasing every ds_read of
@@ -279,6 +300,7 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
     }
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + w * 1024);
     auto issue = [&](int kt, int st) {
+        if (ZK_PF_DIAG_NOFILL) return;
         const uint32_t sa = lds0 + st * ST, sb = sa + AST;
 #pragma unroll
         for (int i = 0; i < NA; ++i) pf_glds_s(abase + kt * BKS, aoff[i], sa + i * 8192);
@@ -288,6 +310,7 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
     constexpr int LPS = NA + NB;                         // LDS-DMA loads per wave and stage
     // one piece j of the stage: activation pieces first, then weight pieces
     auto issue_piece = [&](int kt, int st, int j) {
+        if (ZK_PF_DIAG_NOFILL) return;
         const uint32_t sa = lds0 + st * ST, sb = sa + AST;
         if (j < NA) pf_glds_s(abase + kt * BKS, aoff[j], sa + j * 8192);
         else pf_glds_s(W + (size_t)kt * KSS * 512, boff[j - NA], sb + (j - NA) * 8192);
@@ -308,18 +331,12 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
     for (int s0 = 0; s0 < NSTG - 1; ++s0)
         if (s0 < nk) issue(s0, s0);
     for (int kt = 0; kt < nk; ++kt) {
-        // step kt's copies: everything issued after them may stay in flight
-        const int after = min(NSTG - 2, nk - 1 - kt);
+        // step kt's copies: everything issued after them may stay in flight (with the spread refill every
+        // step issues one stage, clamped past the end, so that is NSTG - 2 stages once the ring is full)
+        const int after = ZK_PF_SPREAD ? min(NSTG - 2, min(NSTG - 1, nk) - 1) : min(NSTG - 2, nk - 1 - kt);
         if constexpr (ZK_PF_DIAG_NOWAIT) {
-        } else if constexpr (NSTG >= 4) {
-            if (after >= 2) pf_vm_wait<2 * LPS>();
-            else if (after == 1) pf_vm_wait<LPS>();
-            else pf_vm_wait<0>();
-        } else if constexpr (NSTG == 3) {
-            if (after >= 1) pf_vm_wait<LPS>();
-            else pf_vm_wait<0>();
         } else {
-            pf_vm_wait<0>();
+            pf_wait_after<LPS, NSTG - 2>(after);
         }
         // the barrier publishes every wave's copies of step kt and ends every read of the stage the
         // refill below overwrites (read in step kt - 1; this wave's reads retired here)
@@ -370,6 +387,15 @@ __global__ __launch_bounds__(PF_NT, 1) void k_gemm_pf(const bf16_t* __restrict__
         }
     }
 
+    if constexpr (ZK_PF_DIAG_NOEPI) {          // (diagnostic: no stores; one lane keeps the sums live)
+        float t = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NTN; ++nt) t += acc[mt][nt][0] + acc[mt][nt][3];
+        if (t == 1.2345f && C) C[0] = t;
+        return;
+    }
     if constexpr (ZK_PF_EPI && (MODE == 1 || NTN == 4)) {
         if (MODE == 1 || N % 4 == 0) {
             pf_epilogue_lds<MODE, NTN>(acc, smem, m0, n0, wr, wc, ln, lg, M, N, C, Cb);
@@ -399,14 +425,17 @@ bool zk_gemm_pf_applies(int M, int N, int K, int nsplit) {
 #ifndef ZK_PF_WIDE
 #define ZK_PF_WIDE 0
 #endif
-constexpr int PF_BKS = ZK_PF_BKS, PF_NSTG = PF_BKS == 64 ? 2 : 4;
+#ifndef ZK_PF_NSTG
+#define ZK_PF_NSTG (ZK_PF_BKS == 64 ? 2 : 4)
+#endif
+constexpr int PF_BKS = ZK_PF_BKS, PF_NSTG = ZK_PF_NSTG;
 constexpr int pf_max(int a, int b) { return a > b ? a : b; }
 template <int MODE, int NTN>
 constexpr int pf_lds() {
     return pf_max(PF_NSTG * (PF_BM + pf_bn<NTN>) * PF_BKS * 2,
                   ZK_PF_EPI ? (MODE == 1 ? pf_epi_lds1<NTN> : pf_epi_lds0<NTN>) : 0);
 }
-static_assert(pf_lds<1, 6>() <= 163840 && pf_lds<0, 4>() <= 163840 && pf_lds<1, 4>() <= 163840, "LDS");
+static_assert((!ZK_PF_WIDE || pf_lds<1, 6>() <= 163840) && pf_lds<0, 4>() <= 163840 && pf_lds<1, 4>() <= 163840, "LDS");
 
 template <int MODE, int NTN>
 static int pf_launch(const void* A, long lda, const void* W, int M, int N, int K, float* C, void* Cb,
