@@ -442,6 +442,9 @@ static int pf_launch(const void* A, long lda, const void* W, int M, int N, int K
                       const int32_t* skip, hipStream_t stream) {
     const long tiles = (long)((M + PF_BM - 1) / PF_BM) * ((N + pf_bn<NTN> - 1) / pf_bn<NTN>);
     ZK_REQUIRE(tiles < (1L << 31), "zk_gemm_bf16 (prefill): too many tiles");
+    // the LDS-DMA sources are 32-bit byte offsets: from the packed weights and from a tile's first row
+    ZK_REQUIRE((long)((N + 63) / 64 * 64) * K * 2 < (1L << 32) && (long)PF_BM * lda * 2 < (1L << 31),
+               "zk_gemm_bf16 (prefill): N=%d K=%d lda=%ld exceed the 32-bit source offsets", N, K, lda);
     auto kern = &k_gemm_pf<MODE, PF_BKS, PF_NSTG, NTN>;
     constexpr int lds = pf_lds<MODE, NTN>();
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
