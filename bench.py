@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--stub", action="store_true", help="CPU stand-in workload (launcher/reporting tests)")
     ap.add_argument("--graph-steps", type=int, default=None,
                     help="decode steps per hipGraph replay (default: the engine's graph_steps)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary measurements after a 1-GPU c3 run (c2, c5, c3 through Zonos.generate)")
     return ap.parse_args()
 
 
@@ -443,6 +445,118 @@ class GpuWorkload:
                                "decode_ms_per_token_step": round(dec_ms, 3)})
 
 
+# ------------------------------------------------------------------------------ secondary configs
+SECONDARY_SP = dict(top_p=0, top_k=0, min_p=0, linear=0.65, conf=0.4, quad=0.0, repetition_penalty=2.5,
+                    repetition_penalty_window=8, temperature=1.0)
+
+
+def _timed_config(torch, dev, generate, dac, B, lc, P, new, reps, warmup, roofline=None, eng=None):
+    """Time `generate(i)` (-> list of [9, T] codes) + the DAC decode of its codes, warmup + reps times,
+    and report the config's codes/s, RTF, decode step time and step roofline like the headline line."""
+    gen_s = dac_s = 0.0
+    frames = 0
+    for i in range(warmup + reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.time()
+        codes = generate(i)
+        torch.cuda.synchronize(dev)
+        t1 = time.time()
+        if dac is not None:
+            dac.decode_list(codes)
+        torch.cuda.synchronize(dev)
+        t2 = time.time()
+        if i >= warmup:
+            gen_s += t1 - t0
+            dac_s += t2 - t1
+            frames += sum(int(c.shape[1]) for c in codes)
+    elapsed = gen_s + dac_s
+    n_dec = new + 8
+    ctx_mean = lc + P + 1 + n_dec // 2
+    dec_ms = gen_s / reps / n_dec * 1e3
+    out = dict(value=round(frames * 9 / elapsed, 1), unit="codes/s", rtf=round(frames / FRAME_RATE / elapsed, 2),
+               reps=reps, warmup=warmup, ms_per_rep=round(elapsed / reps * 1e3, 1),
+               breakdown={"generate_s_per_rep": round(gen_s / reps, 4), "dac_s_per_rep": round(dac_s / reps, 4),
+                          "decode_ms_per_token_step": round(dec_ms, 4)})
+    if eng is not None:
+        sb = step_bytes(eng, 2 * B, ctx_mean)
+        out["step_roofline"] = dict(bytes_per_step=int(sb), ctx_mean=ctx_mean, ms_per_decode_step=round(dec_ms, 4),
+                                    achieved=round(sb / (dec_ms / 1e3) / 1e9, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                                    frac=round(sb / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4))
+    if roofline is not None:
+        out["roofline"] = roofline()
+    return out
+
+
+def secondary_runs(args, wl, headline_value):
+    """after the headline c3 line, on the same box and in the same run,
+    * c2 (BASELINE configs[1]: B = 1, Lc 160, 861 tokens) on the same engine and weights;
+    * c3 through the API callers use -- ``zonos.model.Zonos.generate`` with ``seed=None`` (the
+      reference's torch noise stream), the default poll interval and the tqdm progress bar, DAC via
+      ``model.autoencoder`` -- beside the keyed-engine headline (``generate_sharded``, poll 64);
+    * c5 (configs[4]: the hybrid at B = 64, c3 lengths).
+    Each as codes/s + RTF (generate + DAC decode of all codes, EOS disabled as in the headline),
+    whole-step roofline and the dominant kernel's roofline (HIP events)."""
+    import torch
+
+    from zonos_amd import synthetic
+    from zonos_amd.distributed import generate_sharded
+    dev = wl.dev
+    out = {}
+    t_all = time.time()
+    # --- c2 on the headline engine
+    eng = wl.eng
+    cond2 = synthetic.conditioning(1, 160, 2048, seed=11, device=dev)
+    out["c2"] = dict(workload="c2: B=1, Lc=160, no prefix, 861 new tokens (10 s), EOS disabled, CLI sampling, "
+                              "DAC decode; same engine and weights as the headline",
+                     **_timed_config(torch, dev, lambda i: generate_sharded(
+                         eng, cond2, None, 861, 2.0, 1, wl.sp, seed=2000 + i, force_full_length=True, poll_every=64),
+                         wl.dac, 1, 160, 0, 861, reps=3, warmup=1, roofline=lambda: gemv_roofline(eng), eng=eng))
+    eng.release()
+    wl.eng = None
+    del eng
+    torch.cuda.empty_cache()
+    # --- c3 through Zonos.generate (seed=None: torch's generator stream, poll 16, tqdm)
+    from zonos_amd.autoencoder import DACAutoencoder
+    from zonos_amd.config import BackboneConfig, PrefixConditionerConfig, ZonosConfig
+    from zonos_amd.model import Zonos
+    mc = wl.mc
+    zc = ZonosConfig(BackboneConfig(d_model=mc["d_model"], attn_mlp_d_intermediate=mc["d_ff"], n_layer=mc["n_layer"],
+                                    attn_cfg={"num_heads": mc["n_heads"], "num_heads_kv": mc["n_kv"]}),
+                     PrefixConditionerConfig([], "none"))
+    model = Zonos(zc, synthetic.backbone_weights(dev, seed=0, **mc), dev,
+                  autoencoder=DACAutoencoder(state_dict=synthetic.dac_weights(dev), device=dev))
+    torch.manual_seed(1234)
+    B = args.batch
+    dac = model.autoencoder if wl.dac is not None else None
+    r = _timed_config(torch, dev, lambda i: model.generate(wl.cond, wl.prefix, args.new_tokens, 2.0, B, wl.sp,
+                                                           force_full_length=True),
+                      dac, B, args.lc, args.prefix, args.new_tokens, reps=1, warmup=1, eng=model.engine)
+    out["c3_zonos_generate"] = dict(
+        workload="c3 through zonos.model.Zonos.generate(seed=None): torch's CUDA generator noise (the reference's "
+                 "exponential_ stream), poll every 16 steps, tqdm progress bar; DAC via model.autoencoder.decode_list; "
+                 "force_full_length (EOS disabled) as in the headline",
+        ratio_to_headline=round(r["value"] / headline_value, 4), **r)
+    model.engine.release()
+    del model
+    torch.cuda.empty_cache()
+    # --- c5: the hybrid at B = 64, c3 lengths
+    from zonos_amd.hybrid import HybridDecoder, HybridEngineConfig
+    hc = dict(synthetic.ZONOS_V01_HYBRID)
+    heng = HybridDecoder(HybridEngineConfig(**hc), synthetic.hybrid_weights(dev, seed=0, **hc), dev)
+    out["c5"] = dict(workload="c5: Zonos-v0.1-hybrid (assumed geometry: 46 layers, attention at 9/18/27/36/45, Mamba2 "
+                              "defaults), B=64, Lc=400, prefix 10, 2580 new tokens, EOS disabled, DAC decode",
+                     **_timed_config(torch, dev, lambda i: generate_sharded(
+                         heng, wl.cond, wl.prefix, args.new_tokens, 2.0, B, wl.sp, seed=3000 + i,
+                         force_full_length=True, poll_every=64),
+                         wl.dac, B, args.lc, args.prefix, args.new_tokens, reps=2, warmup=1,
+                         roofline=lambda: mamba_roofline(heng), eng=heng))
+    heng.release()
+    del heng
+    torch.cuda.empty_cache()
+    out["wall_s"] = round(time.time() - t_all, 1)
+    return out
+
+
 def main():
     args = parse()
     rc = launch_ranks(args)
@@ -521,6 +635,9 @@ def main():
         out.update(wl.report(elapsed, args))
         if not args.stub and not args.no_cpu_baseline and world == 1 and args.model == "transformer":
             out["cpu_baseline"] = cpu_baseline(args)
+        if (not args.stub and not args.no_secondary and world == 1 and cfg_name == "c3"
+                and args.model == "transformer" and not args.layers):
+            out["secondary"] = secondary_runs(args, wl, out["value"])
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -322,3 +322,24 @@ def test_root_debug_eos_message_keeps_multistep_polls(caplog):
             msgs.append([r.getMessage() for r in caplog.records if r.getMessage().startswith("Detected EOS")])
     assert msgs[0] and msgs[0] == msgs[1], msgs
     assert all(torch.equal(a, b) for a, b in zip(*outs))
+
+
+@pytest.mark.parametrize("case", ["eos_sampled", "copy_eos"])
+def test_pad_rows_keep_out_of_eos_protocol(case):
+    """generate_sharded pads a short shard with a copy of its last utterance. That
+    row samples its own keyed noise, so left in the batch-wide EOS protocol its EOS would trigger the
+    resample draw of every real row (model.py:380-393) or keep the loop running after they stopped.
+    With pad_rows the padded batch's real rows equal the unpadded batch's codes, lengths included."""
+    from zonos_amd.distributed import _pad_rows
+    c = load_gen_case(case)
+    eng = _engine(c["W"], c["cfg"])
+    B = c["B"]
+    cond, prefix = c["cond"].cuda(), c["prefix"].cuda()
+    ref = eng.generate(cond, prefix, c["max_new"], 2.0, B, c["sp"], seed=c["seed"], poll_every=4)
+    assert any(int(x.shape[1]) < c["max_new"] for x in ref), "the fixture must stop on EOS"
+    condp, prefixp = _pad_rows(cond, B, B + 1, cfg_pairs=True), _pad_rows(prefix, B, B + 1, cfg_pairs=False)
+    got = eng.generate(condp, prefixp, c["max_new"], 2.0, B + 1, c["sp"], seed=c["seed"], poll_every=4,
+                       pad_rows=1)
+    assert len(got) == B + 1
+    for b in range(B):
+        assert torch.equal(got[b], ref[b]), b

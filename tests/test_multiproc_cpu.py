@@ -158,9 +158,11 @@ class RecordingStub(StubEngine):
 
     def __init__(self):
         self.batches = []
+        self.pads = []
 
     def generate(self, cond, prefix, max_new, cfg_scale, B, sp, *, seed, row_base=0, **kw):
         self.batches.append(B)
+        self.pads.append(kw.pop("pad_rows", 0))
         return super().generate(cond, prefix, max_new, cfg_scale, B, sp, seed=seed, row_base=row_base, **kw)
 
 
@@ -175,14 +177,16 @@ def _ragged_worker(rank, world, port, q):
     got = generate_sharded(eng, cond, prefix, 8, 2.0, B, {}, seed=5, coll_device="cpu")
     ref = StubEngine().generate(cond, prefix, 8, 2.0, B, {}, seed=5)
     ok = len(got) == B and all(torch.equal(a, b) for a, b in zip(got, ref))
-    q.put((rank, ok, eng.batches, [gemm_regime(b) for b in eng.batches]))
+    q.put((rank, ok, eng.batches, [gemm_regime(b) for b in eng.batches], eng.pads))
     dist.destroy_process_group()
 
 
 def test_generate_sharded_ragged_keeps_one_regime():
     """B = 17 over 2 ranks is a 9 + 8 split, i.e. M = 18 (k_gemm_ws) beside M = 16
     (k_gemv): two reduction orders. The 8-utterance shard is padded to 9, so both ranks run the
-    k_gemm_ws regime at the same shape, and the gathered codes are still the one-batch codes."""
+    k_gemm_ws regime at the same shape, and the gathered codes are still the one-batch codes. The
+    padding utterance is announced to the engine (pad_rows = 1) so it stays out of the EOS protocol
+    (ADVICE r5; the GPU side: tests/test_gpu_generate.py::test_pad_rows_keep_out_of_eos_protocol)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -195,6 +199,7 @@ def test_generate_sharded_ragged_keeps_one_regime():
     assert all(r[1] for r in res), res
     assert [r[2] for r in res] == [[9], [9]], res
     assert {g for r in res for g in r[3]} == {"ws"}, res
+    assert [r[4] for r in res] == [[0], [1]], res
 
 
 def test_padded_shard_rule():

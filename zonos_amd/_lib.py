@@ -210,6 +210,13 @@ def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def device_index(device) -> int:
+    """The GPU index a (possibly unindexed) cuda device means: torch.device("cuda") is the current
+    device (torch.cuda.set_device), not GPU 0 -- the index of the generator torch itself would use."""
+    device = torch.device(device)
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
 def require_gpu(t: torch.Tensor, name: str = "tensor"):
     if not t.is_cuda:
         raise ZonosHipError(f"{name} must be a GPU tensor (the HIP engine has no CPU path)")

@@ -150,6 +150,8 @@ def generate_sharded(model, prefix_conditioning: torch.Tensor, audio_prefix_code
             cond = _pad_rows(cond, local, run, cfg_pairs=True)
             if prefix is not None:
                 prefix = _pad_rows(prefix, local, run, cfg_pairs=False)
+        if run != local:                 # the padding rows stay out of the EOS protocol (engine.generate)
+            generate_kw = dict(generate_kw, pad_rows=run - local)
         codes = model.generate(cond, prefix, max_new_tokens, cfg_scale, run, sampling_params, seed=seed,
                                row_base=row_base, **generate_kw)[:local]
     if world == 1 or not gather:

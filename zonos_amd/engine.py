@@ -403,7 +403,8 @@ class HipDecoder(HipBackbone):
                  cfg_scale: float = 2.0, batch_size: int = 1, sampling_params: dict | None = None,
                  seed: int = 0, row_base: int = 0, force_full_length: bool = False, callback=None,
                  progress=None, poll_every: int = 16, trace: dict | None = None, use_graph: bool = True,
-                 _after_prefill=None, noise: str = "keyed", generator: torch.Generator | None = None):
+                 _after_prefill=None, noise: str = "keyed", generator: torch.Generator | None = None,
+                 pad_rows: int = 0):
         """Zonos.generate (model.py:224-457). Returns the list of int64 [9, T_i] code tensors.
 
         ``noise`` picks the race noise of the sampler: "keyed" = the engine's stream keyed by
@@ -414,10 +415,18 @@ class HipDecoder(HipBackbone):
         ``torch.manual_seed(s)`` followed by this call leaves torch's RNG where the reference leaves it.
 
         ``trace`` (optional dict) receives per-step fp32 CFG logits (before bias) and the
-        sampled frames -- test instrumentation, forces one step per poll and no graph."""
+        sampled frames -- test instrumentation, forces one step per poll and no graph.
+
+        ``pad_rows``: the last ``pad_rows`` utterances are padding (generate_sharded's uniform shards)
+        whose codes the caller drops. They run through the GEMMs like any row but stay out of the
+        batch-wide EOS protocol (model.py:376-393): they start in EOS mode with no hold-off and no
+        remaining steps, so an EOS they sample never triggers the resample draw of the real rows and
+        never keeps the loop running after the real rows have stopped."""
         assert cfg_scale != 1, "TODO: add support for cfg_scale=1"                     # model.py:247
         if batch_size * 2 != prefix_conditioning.shape[0]:                            # model.py:249-250
             raise ValueError(f"Batch size mismatch: {batch_size} * 2 != {prefix_conditioning.shape[0]}")
+        if not 0 <= pad_rows < batch_size:
+            raise ValueError(f"pad_rows={pad_rows} must leave at least one real utterance of {batch_size}")
         _lib.require_gpu(prefix_conditioning, "prefix_conditioning")
         if prefix_conditioning.dim() != 3 or prefix_conditioning.shape[2] != self.cfg.d_model:
             # zk_prefill copies rows of Lc * d_model bf16: a wrong width would read out of bounds
@@ -449,7 +458,8 @@ class HipDecoder(HipBackbone):
         if noise == "torch":
             if row_base:
                 raise ValueError("noise='torch' is one process's stream (row_base must be 0)")
-            gen = generator if generator is not None else torch.cuda.default_generators[self.device.index or 0]
+            gen = generator if generator is not None else \
+                torch.cuda.default_generators[_lib.device_index(self.device)]
             seed, off0 = int(gen.initial_seed()), int(gen.get_offset())
             stride, incr = zsampling.torch_noise_policy(B * N_CB * VOCAB, self.device)
             st = self._gen_state(ws, B, seed, 0, (1, off0, stride, incr))
@@ -504,6 +514,10 @@ class HipDecoder(HipBackbone):
         ws["stopping"].zero_()
         ws["act"].zero_()
         ws["rp"].fill_(float(spd["repetition_penalty"]))
+        if pad_rows:                        # padding rows: out of the EOS protocol (docstring)
+            ws["eos_mode"][B - pad_rows:] = 1
+            ws["steps_after"][B - pad_rows:] = 0
+            ws["remaining"][B - pad_rows:] = 0
 
         # ---- decode loop (model.py:345-432)
         per_poll = 1 if (callback is not None or trace is not None or logdbg) else max(1, poll_every)

@@ -113,13 +113,19 @@ class Zonos:
                                               repetition_penalty=3.0, repetition_penalty_window=2, temperature=1.0),
                  progress_bar: bool = True, disable_torch_compile: bool = False,
                  callback: Callable[[torch.Tensor, int, int], bool] | None = None, *, seed: int | None = None,
-                 row_base: int = 0, force_full_length: bool = False):
+                 row_base: int = 0, force_full_length: bool = False, pad_rows: int = 0):
         """model.py:224-457. ``disable_torch_compile`` is accepted and ignored (the step is a
         captured hipGraph). Sampling noise: by default (``seed`` None) the reference's own -- every
         sampler call takes the values `torch.empty_like(probs).exponential_(1)` would draw from torch's
         CUDA generator (sampling.py:26-28) and advances that generator as the reference does, so
         ``torch.manual_seed(s)`` (sample.py:19) gives the reference's noise on the same GPU. An
-        integer ``seed`` selects the engine's keyed stream instead (independent of batch sharding)."""
+        integer ``seed`` selects the engine's keyed stream instead (independent of batch sharding).
+
+        ``row_base`` (the global index of this batch's first utterance, for sharded batches) keys the
+        keyed stream only, so it needs an explicit ``seed``: with ``seed=None`` and ``row_base != 0``
+        this raises ValueError. (Before round 5 ``seed=None`` drew a keyed-stream seed from torch and
+        accepted any ``row_base``; ``generate_sharded`` always passes a seed and is unaffected.)
+        ``pad_rows``: trailing padding utterances kept out of the EOS protocol (HipDecoder.generate)."""
         noise = "torch" if seed is None else "keyed"
         if noise == "torch" and row_base:
             raise ValueError("row_base needs an explicit seed (the keyed noise stream)")
@@ -135,7 +141,7 @@ class Zonos:
         out = self.engine.generate(prefix_conditioning.to(self.device), audio_prefix_codes, max_new_tokens,
                                    cfg_scale, batch_size, sampling_params, seed=seed or 0, row_base=row_base,
                                    force_full_length=force_full_length, callback=callback, progress=prog,
-                                   noise=noise)
+                                   noise=noise, pad_rows=pad_rows)
         if prog is not None:
             prog.close()
         return out

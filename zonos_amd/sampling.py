@@ -65,7 +65,11 @@ def sample_from_logits(logits: torch.Tensor, temperature: float = 1.0, top_p: fl
              int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(draw), int(row_base), ptr(out),
              _lib.stream_ptr(lg.device))
         return out
-    g = generator if generator is not None else torch.cuda.default_generators[lg.device.index or 0]
+    if step or draw or row_base:
+        # the keyed stream's coordinates mean nothing to torch's generator stream: refuse them instead
+        # of silently ignoring them (the default changed from the keyed stream to torch's in round 5)
+        raise ValueError("step / draw / row_base select a keyed noise stream: pass seed= with them")
+    g = generator if generator is not None else torch.cuda.default_generators[_lib.device_index(lg.device)]
     stride, incr = torch_noise_policy(B * K * V, lg.device)
     off = int(g.get_offset())
     call("zk_sample_logits_torch", ptr(lg), B, K, V, ptr(gen), gen_len, gen_len, ptr(rp), _lib.C.byref(sp),
