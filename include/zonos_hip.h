@@ -136,9 +136,19 @@ int zk_gemv_fused(const void* A, long lda, const void* W, int M, int N, int K, i
  * partials of zk_attn_decode_qkv_part: x[M][N] = bf16(x + bf16(merge(work) . W^T))
  * (_torch.py:66 + the residual add of :100), the merge being k_attn_combine's arithmetic
  * (bit-identical to zk_attn_decode_qkv + zk_gemv_fused mode 2 with the same nsplit).
- * K = 2048 (16 heads x 128), nsplit in {2, 4, 8}. */
+ * K = 2048 (16 heads x 128), nsplit in {2, 4, 8, 16}. Also the consumer of zk_attn_decode_q_part. */
 int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const void* W, int M, int N, int K,
                      void* x, const int32_t* skip, void* stream);
+/* in_proj of the B = 1 decode layer (M = 2 rows) with the RoPE / KV-write epilogue
+ * (_torch.py:61-65 + apply_rotary_emb :18-30 + _update_kv_cache :33-49): LayerNorm(x) (ln_w, ln_b,
+ * the norm prologue of zk_gemv_fused) . Wqkv^T, each column rounded to bf16, q and k rotated by the
+ * interleaved RoPE pairs at position p = min(*pos_dev, Smax - 1) (freqs as zk_qkv_rope), q stored to
+ * q_out bf16 [M][H*hd], k and v written into the layer's cache at key p (layout of zk_qkv_rope).
+ * Bit-identical to zk_gemv_fused mode 0 + the fused prologue of zk_attn_decode_qkv. d_model = H*hd =
+ * 2048, hd = 128. */
+int zk_gemv_qkv_rope(const void* x, const void* W, int M, int H, int Hkv, int hd, const void* ln_w,
+                     const void* ln_b, float eps, void* q_out, void* k_cache, void* vt_cache, int Smax,
+                     const int32_t* pos_dev, const float* freqs, const int32_t* skip, void* stream);
 /* fc1 weight [2F][D] (rows: F "y" then F "gate") -> interleaved groups of 8 y + 8 gate rows. */
 int zk_permute_fc1(const void* w_fc1, int F, int D, void* w_out, void* stream);
 /* nn.Linear weight [N][K] bf16 -> fragment-packed [ceil64(N)/16][K/32][64][8] (rows >= N zero):
@@ -202,6 +212,15 @@ int zk_attn_decode_qkv_part(const float* part, int gemm_nsplit, const float* fre
                             const int32_t* ctx_dev, float* work, int nsplit, int rope_neox,
                             const int32_t* skip, void* stream);
 
+/* Decode attention of the B = 1 step when q and the new key / value come from zk_gemv_qkv_rope:
+ * F.scaled_dot_product_attention of one query per row over keys [0, ctx), ctx = min(ctx0 + *ctx_dev,
+ * Smax) (_torch.py:64-65), with the keys split in 32-key slices over nsplit workgroups per (row, kv
+ * head) (workgroup s, wave w: slices 4s + w + 4 nsplit j). Leaves the partials (m, l, unnormalised O)
+ * in work [R][Hkv][nsplit][8 + 4*128] fp32 for zk_gemv_attn_out. nsplit <= 64. */
+int zk_attn_decode_q_part(const void* q, const void* k_cache, const void* vt_cache, int R, int H, int Hkv,
+                          int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work, int nsplit,
+                          const int32_t* skip, void* stream);
+
 /* ------------------------------------------------------------------ graphs and timing
  * The decode step is captured once into a hipGraph and replayed (the reference runs the
  * transformer step eagerly: model.py:138-142, 220-222). */
@@ -261,7 +280,8 @@ int zk_eos_step(const zk_gen_state* st, int prefill, int prefix_len, void* strea
  * delayed-frame write) enqueued on `stream` with no host synchronisation, exactly the launch
  * sequence of zonos_amd.engine.HipDecoder._decode_step (the Python engine calls this entry):
  * small = 1 (B <= 8): five launches per block (zk_gemv_fused LayerNorm prologues / residual
- * epilogues; attn_merge > 0: zk_attn_decode_qkv_part + zk_gemv_attn_out); small = 0: seven
+ * epilogues; attn_merge > 0: zk_gemv_qkv_rope + zk_attn_decode_q_part + zk_gemv_attn_out, or with
+ * rope_neox zk_gemv_fused + zk_attn_decode_qkv_part + zk_gemv_attn_out); small = 0: seven
  * (split-K zk_gemm_bf16 + zk_attn_decode_qkv_sc + zk_resid_ln). Every position/offset is read
  * from st.scal on the device, so one call is captured once into a hipGraph and replayed.
  * Replaces the per-token Python loop body of model.py:322-424 for a C/C++ host. */

@@ -40,6 +40,10 @@ STUB(zk_attn_decode_qkv_sc, const float*, int, const float*, void*, void*, int, 
      const int32_t*, float*, int, uint32_t*, void*, int, const int32_t*, void*)
 STUB(zk_attn_decode_qkv_part, const float*, int, const float*, void*, void*, int, int, int, int, int, int,
      const int32_t*, float*, int, int, const int32_t*, void*)
+STUB(zk_gemv_qkv_rope, const void*, const void*, int, int, int, int, const void*, const void*, float, void*, void*,
+     void*, int, const int32_t*, const float*, const int32_t*, void*)
+STUB(zk_attn_decode_q_part, const void*, const void*, const void*, int, int, int, int, int, int, const int32_t*, float*,
+     int, const int32_t*, void*)
 STUB(zk_sample_heads, const float*, int, const zk_gen_state*, const zk_sampling_params*, int, int, float*, void*)
 STUB(zk_eos_step, const zk_gen_state*, int, int, void*)
 STUB(zk_mamba_step, const float*, int, int, int, int, int, int, const float*, const float*, void*, void*,
@@ -126,6 +130,11 @@ static void transformer(int n_layer, int small, int merge) {
     CHECK(count("zk_sample_heads") == 2 && count("zk_eos_step") == 1, "decode tail");
     if (!small) CHECK(count("zk_resid_ln") == (size_t)2 * n_layer, "resid_ln x2 per layer");
     if (small && merge) CHECK(count("zk_gemv_attn_out") == (size_t)n_layer, "merged out_proj per layer");
+    // B = 1 with merged splits: the in_proj RoPE epilogue + the prologue-free attention
+    if (small && merge)
+        CHECK(count("zk_gemv_qkv_rope") == (size_t)n_layer && count("zk_attn_decode_q_part") == (size_t)n_layer &&
+                  count("zk_attn_decode_qkv_part") == 0,
+              "B = 1 layer sequence");
     // prefill
     g_calls.clear();
     g_warm = 0;

@@ -103,7 +103,9 @@ def test_attention_split_rule():
     """Flash-decoding key splits: none at B=64 (512 workgroups already), and each split covers
     >= 2048 cached keys (a combine launch costs more than it saves below that)."""
     from zonos_amd.engine import attn_merge_for, attn_splits_for
-    assert attn_merge_for(2, 1280) == 4 and attn_merge_for(2, 256) == 2 and attn_merge_for(2, 128) == 0
+    # B = 1: 4 splits of 32-key slices at every cache size (round-6 A/B, c2 decode step at
+    # 2 / 4 / 8 splits: 0.975-0.978 / 0.959-0.962 / 0.977-0.980 ms, profiles/r6_c2_split_ab.txt)
+    assert attn_merge_for(2, 1280) == 4 and attn_merge_for(2, 256) == 4 and attn_merge_for(1 * 2, 3328) == 4
     assert attn_merge_for(4, 1280) == 0 and attn_merge_for(128, 3072) == 0
     assert attn_splits_for(128, 4, 3072) == 1           # c3
     assert attn_splits_for(2, 4, 1280) == 1             # c2: B=1, 10 s

@@ -480,3 +480,92 @@ def test_attention_out_proj_merge(R, ctx, nsplit):
     assert torch.equal(x1.view(torch.int16), x2.view(torch.int16)), (x1.float() - x2.float()).abs().max()
     # and the result is the attention + projection of an fp32 reference within bf16 tolerance
     assert not torch.equal(x1, x0)
+
+
+@pytest.mark.parametrize("M,pos,smax", [(2, 0, 256), (2, 31, 256), (2, 32, 512), (1, 600, 1280), (2, 1029, 1280),
+                                        (2, 5000, 1280)])
+def test_gemv_qkv_rope_equals_gemv_and_rope(M, pos, smax):
+    """zk_gemv_qkv_rope (the B = 1 in_proj with the RoPE / KV-write epilogue) == zk_gemv_fused mode 0
+    with the LayerNorm prologue + zk_qkv_rope at the same position, bit for bit: q and every cache
+    byte (a position past the cache is clamped to Smax - 1, as the attention clamps its context)."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import pack_weights, rope_table
+    H, Hk, hd, D = 16, 4, 128, 2048
+    N = (H + 2 * Hk) * hd
+    g = torch.Generator(device="cpu").manual_seed(pos * 3 + M)
+    s = stream_ptr()
+    x = torch.randn(M, D, generator=g).to(torch.bfloat16).to(DEV)
+    Wpk = pack_weights((torch.randn(N, D, generator=g) / D ** 0.5).to(torch.bfloat16).to(DEV), s)
+    lw = (1 + 0.1 * torch.randn(D, generator=g)).to(torch.bfloat16).to(DEV)
+    lb = (0.1 * torch.randn(D, generator=g)).to(torch.bfloat16).to(DEV)
+    freqs = rope_table(16384, hd).to(DEV)
+    kc0 = torch.randn(M * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    vt0 = torch.randn(M * Hk * smax * hd, generator=g).to(torch.bfloat16).to(DEV)
+    p = min(pos, smax - 1)
+    part = torch.empty(M, N, device=DEV)
+    call("zk_gemv_fused", ptr(x), D, ptr(Wpk), M, N, D, 0, ptr(lw), ptr(lb), 1e-5, ptr(part), None, None, s)
+    q1 = torch.empty(M, H * hd, dtype=torch.bfloat16, device=DEV)
+    kc1, vt1 = kc0.clone(), vt0.clone()
+    call("zk_qkv_rope", ptr(part), 1, M, 1, H, Hk, hd, ptr(freqs), p, None, ptr(q1), ptr(kc1), ptr(vt1), smax, None,
+         0, None, s)
+    q2 = torch.full((M, H * hd), float("nan"), dtype=torch.bfloat16, device=DEV)
+    kc2, vt2 = kc0.clone(), vt0.clone()
+    posd = torch.tensor([pos], dtype=torch.int32, device=DEV)
+    call("zk_gemv_qkv_rope", ptr(x), ptr(Wpk), M, H, Hk, hd, ptr(lw), ptr(lb), 1e-5, ptr(q2), ptr(kc2), ptr(vt2), smax,
+         ptr(posd), ptr(freqs), None, s)
+    torch.cuda.synchronize()
+    assert torch.equal(q1.view(torch.int16), q2.view(torch.int16))
+    assert torch.equal(kc1, kc2) and torch.equal(vt1, vt2)
+    assert not torch.equal(kc1, kc0) and not torch.equal(vt1, vt0)
+    # skipped (done word set): nothing is written
+    done = torch.ones(1, dtype=torch.int32, device=DEV)
+    kc3, vt3 = kc0.clone(), vt0.clone()
+    q3 = q2.clone()
+    call("zk_gemv_qkv_rope", ptr(x), ptr(Wpk), M, H, Hk, hd, ptr(lw), ptr(lb), 1e-5, ptr(q3), ptr(kc3), ptr(vt3), smax,
+         ptr(posd), ptr(freqs), ptr(done), s)
+    torch.cuda.synchronize()
+    assert torch.equal(kc3, kc0) and torch.equal(vt3, vt0) and torch.equal(q3.view(torch.int16), q2.view(torch.int16))
+
+
+@pytest.mark.parametrize("R,ctx,nsplit", [(2, 1, 8), (2, 31, 4), (2, 33, 8), (2, 600, 4), (2, 600, 8), (1, 1000, 16),
+                                          (2, 1030, 16), (2, 257, 2)])
+def test_attention_q_part_out_proj_merge(R, ctx, nsplit):
+    """zk_attn_decode_q_part (32-key slices interleaved over nsplit workgroups per (row, kv head)) +
+    zk_gemv_attn_out == the unsplit zk_attn_decode + zk_gemv_fused mode 2 up to the fp32 summation
+    order of the split merge (the residual stream after out_proj within 1 bf16 ulp; measured: up to 6 %
+    of its elements one ulp apart),
+    and the attention itself against an fp32 SDPA of the same cache."""
+    from zonos_amd._lib import call, ptr, stream_ptr
+    from zonos_amd.engine import pack_weights
+    H, Hk, hd, D = 16, 4, 128, 2048
+    smax = ((ctx + 255) // 256) * 256
+    k, v, kc, vt = _attn_setup(R, ctx, H, Hk, hd, smax, seed=ctx + nsplit)
+    g = torch.Generator(device="cpu").manual_seed(ctx * 5 + nsplit)
+    q = torch.randn(R, H * hd, generator=g).to(torch.bfloat16)
+    s = stream_ptr()
+    Wo = pack_weights((torch.randn(D, H * hd, generator=g) * 0.02).to(torch.bfloat16).to(DEV), s)
+    x0 = torch.randn(R, D, generator=g).to(torch.bfloat16).to(DEV)
+    qd, kd, vd = q.to(DEV), kc.to(DEV), vt.to(DEV)
+    ctxd = torch.tensor([ctx - 1], dtype=torch.int32, device=DEV)       # ctx = ctx0 (1) + *ctx_dev
+    y = torch.empty(R, H * hd, dtype=torch.bfloat16, device=DEV)
+    call("zk_attn_decode", ptr(qd), ptr(kd), ptr(vd), R, H, Hk, hd, smax, ctx, None, None, 1, ptr(y), None, s)
+    x1 = x0.clone()
+    call("zk_gemv_fused", ptr(y), H * hd, ptr(Wo), R, D, H * hd, 2, None, None, 1e-5, None, ptr(x1), None, s)
+    work = torch.full((R * Hk * nsplit * (8 + 4 * hd),), float("nan"), device=DEV)
+    call("zk_attn_decode_q_part", ptr(qd), ptr(kd), ptr(vd), R, H, Hk, hd, smax, 1, ptr(ctxd), ptr(work), nsplit,
+         None, s)
+    x2 = x0.clone()
+    call("zk_gemv_attn_out", ptr(work), nsplit, Hk, ptr(Wo), R, D, H * hd, ptr(x2), None, s)
+    torch.cuda.synchronize()
+    assert torch.isfinite(x2.float()).all()
+    err = (x2.float() - x1.float()).abs()
+    assert err.max() < 0.07 and (err > 0).float().mean() < 0.15, (err.max(), (err > 0).float().mean())
+    # the merged attention itself (from the partials) vs an fp32 SDPA
+    wk = work.view(R, Hk, nsplit, 8 + 4 * hd).cpu()
+    m, l, o = wk[..., :4], wk[..., 4:8], wk[..., 8:].view(R, Hk, nsplit, 4, hd)
+    M_ = m.max(dim=2, keepdim=True).values
+    c = torch.where(m == -float("inf"), torch.zeros_like(m), torch.exp(m - M_))
+    att = (o * c[..., None]).sum(2) / (l * c).sum(2)[..., None]
+    ref = F.scaled_dot_product_attention(q.view(R, 1, H, hd).transpose(1, 2).float(), k.transpose(1, 2).float(),
+                                         v.transpose(1, 2).float(), enable_gqa=True).view(R, Hk, 4, hd)
+    assert (att - ref).abs().max() < 2e-2

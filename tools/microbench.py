@@ -358,6 +358,51 @@ def gemv():
     print(f"gemv total per layer-ish: fused {tot_new:.1f} us, old {tot_old:.1f} us", flush=True)
 
 
+def gemv_warm():
+    """Experiment: B = 1 GEMV launches (zk_gemv_fused at M = 2, the c2 layouts) whose first weight
+    loads per wave were just pre-read into L2 by zk_gemv_warm (same grid and addresses) vs cold; the
+    GEMV after the warm-up = time(pair) - time(warm alone). Rotating weight copies (> MALL)."""
+    lib = _lib.load()
+    lib.zk_gemv_warm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    M, D = 2, 2048
+    x = torch.randn(M, 8192, device=dev).to(torch.bfloat16)
+    lw = torch.ones(D, device=dev, dtype=torch.bfloat16)
+    lb = torch.zeros(D, device=dev, dtype=torch.bfloat16)
+    outf = torch.empty(M * 16384, device=dev)
+    outb = torch.empty(M * 16384, device=dev, dtype=torch.bfloat16)
+    res = torch.randn(M, D, device=dev).to(torch.bfloat16)
+    # name, N, K, mode, LN, layout (zk_gemv_fused: lay 0 half tiles / 1 one tile / 2 two tiles), loads per wave
+    for name, N, K, mode, ln, lay, nl in (("qkv", 3072, 2048, 0, True, 1, 16), ("o", 2048, 2048, 2, False, 0, 4),
+                                          ("fc1", 16384, 2048, 1, True, 2, 16), ("fc2", 2048, 8192, 2, False, 0, 16)):
+        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
+        Npad = (N + 63) // 64 * 64
+        Ws = [torch.randn(Npad, K, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+        it = [0]
+
+        def g():
+            W = Ws[it[0] % ncopy]; it[0] += 1
+            call("zk_gemv_fused", ptr(x), K, ptr(W), M, N, K, mode, ptr(lw) if ln else None, ptr(lb) if ln else None,
+                 1e-5, ptr(outf), ptr(res) if mode == 2 else ptr(outb), None, S)
+        tc = timeit(g)
+        for steps in sorted({2, 4, 8, nl}):
+            if steps > nl:
+                continue
+
+            def wg():
+                W = Ws[it[0] % ncopy]; it[0] += 1
+                assert lib.zk_gemv_warm(ptr(W), N, K, lay, steps, S) == 0
+
+            def pair():
+                W = Ws[it[0] % ncopy]; it[0] += 1
+                assert lib.zk_gemv_warm(ptr(W), N, K, lay, steps, S) == 0
+                call("zk_gemv_fused", ptr(x), K, ptr(W), M, N, K, mode, ptr(lw) if ln else None,
+                     ptr(lb) if ln else None, 1e-5, ptr(outf), ptr(res) if mode == 2 else ptr(outb), None, S)
+            tw, tp = timeit(wg), timeit(pair)
+            print(f"gemv_warm {name:4s} steps {steps:2d}/{nl}: cold {tc:6.2f} us, warm kernel {tw:5.2f}, pair {tp:6.2f}"
+                  f" -> gemv after warm-up {tp - tw:6.2f} us", flush=True)
+        del Ws
+
+
 def dac():
     from zonos_amd import synthetic
     from zonos_amd.autoencoder import DacSpec, HipDacDecoder
@@ -385,6 +430,8 @@ if __name__ == "__main__":
         attn_small()
     if what in ("gemv",):
         gemv()
+    if what == "gemv_warm":
+        gemv_warm()
     if what in ("prefill", "all"):
         prefill()
     if what in ("ln", "all"):

@@ -107,6 +107,8 @@ _SIGS = {
     "zk_attn_decode_qkv_sc": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, P, P, I, P, P],
     "zk_attn_decode_qkv_part": [P, I, P, P, P, I, I, I, I, I, I, P, P, I, I, P, P],
     "zk_gemv_attn_out": [P, I, I, P, I, I, I, P, P, P],
+    "zk_gemv_qkv_rope": [P, P, I, I, I, I, P, P, F, P, P, P, I, P, P, P, P],
+    "zk_attn_decode_q_part": [P, P, P, I, I, I, I, I, I, P, P, I, P, P],
     "zk_decode_step": [C.POINTER(StepDesc), P],
     "zk_prefill": [C.POINTER(StepDesc), P, I, I, P, P],
     "zk_hybrid_decode_step": [C.POINTER(HybridDesc), P],

@@ -467,6 +467,112 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
     }
 }
 
+// B = 1 decode attention over 32-key slices (zk_attn_decode_q_part): q comes from the in_proj GEMV's
+// RoPE epilogue (zk_gemv_qkv_rope), which also wrote the new key / value into the cache, so there is no
+// prologue: the q fragments and the step words are loaded at entry, the first slice as soon as the
+// context is known. Workgroup (split, kv head g, row r), wave w takes the slices split * 4 + w + j * 4 *
+// nsplit (interleaved, so every split gets an equal share at any context and all 4 * nsplit waves of a
+// (row, kv head) start with one slice), two slices in flight; the 4 waves merge through LDS and the
+// workgroup writes its (m, l, O) partial, which the out_proj GEMV merges (zk_gemv_attn_out).
+template <bool KVNT>
+__global__ __launch_bounds__(256, 2) void k_attn_decode_qs(const bf16_t* q, const bf16_t* kc, const bf16_t* vt,
+                                                           int H, int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
+                                                           float* work, float scale, const int32_t* skip) {
+    constexpr int HD = 128;
+    __shared__ AttnSmem sm;
+    const int split = blockIdx.x, nsplit = gridDim.x, g = blockIdx.y, r = blockIdx.z;
+    const int G = H / Hkv;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ln = lane & 15, lg = lane >> 4;
+    ZK_ATT_STAMP(0);
+    const int sk = ld_word(skip);
+    const int cw = ld_word(ctx_dev);
+    // q fragments (B operand of S^T = K.Q^T: lane ln < G holds head g*G + ln), independent of the context
+    const bf16_t* qr = q + (size_t)r * H * HD + (size_t)(g * G + min(ln, G - 1)) * HD;
+    uint4 qv[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qv[ks] = *reinterpret_cast<const uint4*>(qr + ks * 32 + lg * 8);
+    const bf16_t* kb = kc + ((size_t)r * Hkv + g) * Smax * HD;
+    const bf16_t* vb = vt + ((size_t)r * Hkv + g) * HD * (size_t)Smax;
+    const int step = 4 * nsplit;
+    const int s0 = split * 4 + w;
+    // the wave's first slice is loaded before the context is known (in bounds: clamped to the cache;
+    // unused when the context ends before it), so the context word's round trip overlaps it
+    // (loading its second slice speculatively as well measured slower: the CU's load issue, 64 KB per
+    // workgroup and slice, then holds back the context word's test, profiles/r6_c2_attn_stamps.txt)
+    KVFrag fa, fb;
+    load_kv<KVNT>(fa, kb, vb, Smax, min(s0, Smax / 32 - 1) * 32, ln, lg);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);       // (the wait for the context word below, not above these loads)
+    const int ctx = min(ctx0 + uni(cw), Smax);
+    ZK_ATT_STAMP(1);
+    const int nsl = (ctx + 31) >> 5;
+    if (s0 + step < nsl) load_kv<KVNT>(fb, kb, vb, Smax, (s0 + step) * 32, ln, lg);
+    if (uni(sk) != 0) {        // skip: nothing is written (the loads above are in bounds)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) { keep_live(fa.k[h][ks]); keep_live(fb.k[h][ks]); }
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) { keep_live(fa.v[dt]); keep_live(fb.v[dt]); }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) keep_live(qv[ks]);
+        return;
+    }
+    bf16x8 qf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = as_frag(ln < G ? qv[ks] : make_uint4(0, 0, 0, 0));
+    AttnState st;
+    st.m = -INFINITY;
+    st.l = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = s0; s < nsl; s += 2 * step) {
+        attn_step(st, fa, qf, s * 32, ctx, scale, lg);
+        if (s == s0) ZK_ATT_STAMP(2);
+        if (s + 2 * step < nsl) load_kv<KVNT>(fa, kb, vb, Smax, (s + 2 * step) * 32, ln, lg);
+        if (s + step < nsl) {
+            attn_step(st, fb, qf, (s + step) * 32, ctx, scale, lg);
+            if (s + 3 * step < nsl) load_kv<KVNT>(fb, kb, vb, Smax, (s + 3 * step) * 32, ln, lg);
+        }
+    }
+    ZK_ATT_STAMP(3);
+    // merge the 4 waves with one barrier: each wave leaves its unscaled (m, l, O) in LDS and every thread
+    // combines its (head, dim) items -- the products and the wave order of attn_decode_wg's two-barrier
+    // merge (O_w * exp(m_w - M), summed w = 0..3), so the same numbers
+    if (lg == 0) { sm.s_m[w][ln] = st.m; sm.s_l[w][ln] = st.l; }
+    if (ln < AT_G) {
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sm.s_o[w][ln][dt * 16 + lg * 4 + i] = st.o[dt][i];
+    }
+    __syncthreads();
+    ZK_ATT_STAMP(4);
+    float* wp = work + (((size_t)r * Hkv + g) * nsplit + split) * AT_STR;
+    for (int i = threadIdx.x; i < AT_G * HD; i += 256) {
+        const int h = i / HD, d = i % HD;
+        const float Mh = fmaxf(fmaxf(sm.s_m[0][h], sm.s_m[1][h]), fmaxf(sm.s_m[2][h], sm.s_m[3][h]));
+        float o = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float c = (sm.s_m[k][h] == -INFINITY) ? 0.f : __expf(sm.s_m[k][h] - Mh);
+            o = k == 0 ? sm.s_o[0][h][d] * c : o + sm.s_o[k][h][d] * c;
+        }
+        wp[2 * AT_G + i] = o;
+    }
+    if (threadIdx.x < AT_G) {
+        const int h = threadIdx.x;
+        float Mh = -INFINITY;
+        for (int k = 0; k < 4; ++k) Mh = fmaxf(Mh, sm.s_m[k][h]);
+        float L = 0.f;
+        for (int k = 0; k < 4; ++k) L += (sm.s_m[k][h] == -INFINITY) ? 0.f : sm.s_l[k][h] * __expf(sm.s_m[k][h] - Mh);
+        wp[h] = Mh;
+        wp[AT_G + h] = L;
+    }
+    ZK_ATT_STAMP(5);
+}
+
 template <bool FUSED, bool NEOX, bool KVNT, bool COMB = false>
 __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H,
                                                         int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,

@@ -715,6 +715,24 @@ extern "C" int zk_attn_decode_qkv_part(const float* part, int gemm_nsplit, const
     return 0;
 }
 
+extern "C" int zk_attn_decode_q_part(const void* q, const void* k_cache, const void* vt_cache, int R, int H,
+                                     int Hkv, int hd, int Smax, int ctx0, const int32_t* ctx_dev, float* work,
+                                     int nsplit, const int32_t* skip, void* stream) {
+    ZK_REQUIRE(hd == 128, "zk_attn_decode_q_part: head_dim %d unsupported (128 only)", hd);
+    ZK_REQUIRE(H % Hkv == 0 && H / Hkv <= AT_G, "zk_attn_decode_q_part: GQA group %d > %d", H / Hkv, AT_G);
+    ZK_REQUIRE(Smax % 32 == 0 && Smax > 0, "zk_attn_decode_q_part: Smax=%d must be a multiple of 32", Smax);
+    ZK_REQUIRE(nsplit >= 1 && nsplit <= 64, "zk_attn_decode_q_part: nsplit=%d out of [1, 64]", nsplit);
+    ZK_REQUIRE(q != nullptr && work != nullptr && k_cache != nullptr && vt_cache != nullptr,
+               "zk_attn_decode_q_part: null buffer");
+    const float scale = 1.0f / sqrtf((float)hd);
+    const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
+    auto kern = kvnt ? k_attn_decode_qs<true> : k_attn_decode_qs<false>;
+    hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q,
+                       (const bf16_t*)k_cache, (const bf16_t*)vt_cache, H, Hkv, Smax, ctx0, ctx_dev, work, scale, skip);
+    ZK_CHECK_LAUNCH("zk_attn_decode_q_part");
+    return 0;
+}
+
 extern "C" int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
                                      void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
                                      const int32_t* ctx_dev, float* work, int nsplit, uint32_t* counters, void* out,

@@ -134,6 +134,12 @@ static ZkWarm warm_desc(const void* W, int M, int N, int K, int nsplit, int mode
     return ZK_L2_WARM ? zk_gemm_warm_desc(W, M, N, K, nsplit, mode, 2) : ZkWarm{nullptr, 0, 0, 0, 0};
 }
 
+// B = 1: RoPE + KV write in the in_proj epilogue and the prologue-free attention (round 6);
+// ZK_B1_QKV_EPI=0 builds the round-5 sequence (in_proj slab -> fused-prologue attention) for A/Bs
+#ifndef ZK_B1_QKV_EPI
+#define ZK_B1_QKV_EPI 1
+#endif
+
 extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
     if (d == nullptr || d->layers == nullptr || d->n_layer <= 0 || d->B <= 0) {
         zk_set_error("zk_decode_step: bad descriptor");
@@ -153,7 +159,19 @@ extern "C" int zk_decode_step(const zk_step_desc* d, void* stream) {
                            d->small ? nullptr : d->xn, skip, stream));
     for (int i = 0; i < d->n_layer; ++i) {
         const zk_step_layer& L = d->layers[i];
-        if (d->small) {
+        if (ZK_B1_QKV_EPI && d->small && d->attn_merge > 0 && !d->rope_neox) {
+            // B = 1: RoPE + KV write in the in_proj epilogue, a prologue-free attention over 32-key
+            // slices, its partials merged by the out_proj GEMV
+            ZK_STEP(zk_gemv_qkv_rope(d->x, L.wqkv, R, H, Hk, hd, L.ln1_w, L.ln1_b, d->eps, d->y, L.k_cache,
+                                     L.vt_cache, d->smax, pos, d->freqs, skip, stream));
+            ZK_STEP(zk_attn_decode_q_part(d->y, L.k_cache, L.vt_cache, R, H, Hk, hd, d->smax, 1, pos, d->attn_work,
+                                          d->attn_merge, skip, stream));
+            ZK_STEP(zk_gemv_attn_out(d->attn_work, d->attn_merge, Hk, L.wo, R, D, H * hd, d->x, skip, stream));
+            ZK_STEP(zk_gemv_fused(d->x, D, L.fc1, R, 2 * Fd, D, 1, L.ln2_w, L.ln2_b, d->eps, nullptr, d->h, skip,
+                                  stream));
+            ZK_STEP(zk_gemv_fused(d->h, Fd, L.fc2, R, D, Fd, 2, nullptr, nullptr, d->eps, nullptr, d->x, skip,
+                                  stream));
+        } else if (d->small) {
             ZK_STEP(zk_gemv_fused(d->x, D, L.wqkv, R, Nqkv, D, 0, L.ln1_w, L.ln1_b, d->eps, d->part, nullptr, skip,
                                   stream));
             if (d->attn_merge > 0) {

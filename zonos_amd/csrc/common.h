@@ -28,6 +28,15 @@ ZK_DEV int32_t ld_word_here(const int32_t* p) {
     asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(q) : "memory");
     return v;
 }
+// Two step words by scalar loads issued here and waited for together (one round trip).
+ZK_DEV void ld_words_here(const int32_t* p0, const int32_t* p1, int32_t& v0, int32_t& v1) {
+    const int32_t* q0 = p0 != nullptr ? p0 : &zk_zero_word;
+    const int32_t* q1 = p1 != nullptr ? p1 : &zk_zero_word;
+    asm volatile("s_load_dword %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(v0), "=&s"(v1)
+                 : "s"(q0), "s"(q1)
+                 : "memory");
+}
 // Use of loaded registers on a kernel's early-exit path: without a use there, hipcc sinks the
 // loads into the path that consumes them, i.e. below the exit test, which then waits for the
 // step word before the first data load is issued.

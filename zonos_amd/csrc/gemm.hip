@@ -656,6 +656,20 @@ __global__ __launch_bounds__(256, 1) void k_gemv_rk(const bf16_t* __restrict__ A
 // workgroup -- 4 of the 8 128-B lines of every 1 KB fragment each) so N = 2048 still gives
 // 256 workgroups.
 // mode 0: fp32 Cf[M][N]; mode 1: SwiGLU -> bf16 Cb[M][N/2]; mode 2: residual, Cb = x bf16 [M][N].
+// ZK_GF_PROF (profiling builds only): lane 0 of wave 0 of each k_gemv_f workgroup writes s_memrealtime
+// stamps [entry, first MFMA issued, last MFMA issued, end] to g_gf_prof[slot][blockIdx.x][k], slot =
+// 2 * MODE + (MRG > 0) (so the launches of one kind in a step overwrite each other: the last one stays).
+#ifdef ZK_GF_PROF
+__device__ uint64_t* g_gf_prof;
+#define ZK_GF_STAMP(k)                                                                                      \
+    do {                                                                                                    \
+        if (threadIdx.x == 0 && g_gf_prof)                                                                  \
+            g_gf_prof[((size_t)(2 * MODE + (MRG > 0)) * 2048 + blockIdx.x) * 4 + (k)] =                     \
+                __builtin_amdgcn_s_memrealtime();                                                           \
+    } while (0)
+#else
+#define ZK_GF_STAMP(k) do {} while (0)
+#endif
 ZK_DEV void opaque(uint4& v) {
     u32x4 t = __builtin_bit_cast(u32x4, v);
     asm volatile("" : "+v"(t));
@@ -681,13 +695,29 @@ static_assert(GF_AT_STR == 2 * GF_AT_G + GF_AT_G * 128, "attention partials layo
 #ifndef ZK_GF_OCC2
 #define ZK_GF_OCC2 1               // min waves per SIMD the B = 1 (XR = 2) instantiations are sized for
 #endif
+// mode 3 (in_proj of the B = 1 step): the epilogue of the decode attention's old prologue. The GEMV
+// output is final (no split-K), so each column pair (2j, 2j+1) of a q / k head -- two neighbouring lanes
+// of one 16-column tile -- is rounded to bf16 and rotated here (interleaved RoPE, _torch.py:18-30, the
+// arithmetic of k_qkv_rope / attn_decode_wg's prologue), q is stored to Cb [M][H*hd] and the new key /
+// value straight into the fragment-ordered KV cache at position *pos, so the attention kernel reads q
+// and the whole cache and has no prologue.
+struct GfQkv {
+    bf16_t* kc;            // K cache of the layer ([row][kv head] blocks of Smax * 128)
+    bf16_t* vt;            // V^T cache
+    const int32_t* pos;    // device position word (= context - 1 of this step)
+    const float* freqs;    // [pos][64][2] (cos, sin)
+    int H, Hkv, Smax;
+};
+
 template <int MODE, bool LN, int NTW, bool HALF, int NW, int KS, int PF, int MRG = 0, int XR = 16>
 __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(const bf16_t* __restrict__ A, long lda,
                                                        const bf16_t* __restrict__ W, int M, int N, int K,
                                                        const bf16_t* __restrict__ lnw, const bf16_t* __restrict__ lnb,
                                                        float eps, float* __restrict__ Cf, bf16_t* __restrict__ Cb,
                                                        const int32_t* skip, const float* __restrict__ mw = nullptr,
-                                                       int mhkv = 1) {
+                                                       int mhkv = 1, GfQkv qk = GfQkv{}) {
+    static_assert(MODE != 3 || (LN && NTW == 1 && !HALF && XR == 2), "qkv RoPE epilogue: the B = 1 in_proj");
+    ZK_GF_STAMP(0);
     static_assert(!HALF || NTW == 1, "HALF is one half tile");
     static_assert(!LN || KS * NW * 32 == 2048, "LN prologue: K = 2048");
     static_assert(!MRG || (!LN && NW == 8 && KS * NW * 32 == 2048), "merge prologue: K = 2048, 8 waves");
@@ -728,27 +758,31 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
             for (int j = 0; j < NJ; ++j)
                 xv[rr][j] = *reinterpret_cast<const uint4*>(A + (size_t)min(w + NW * rr, M - 1) * lda + lane * 8 + j * 512);
     }
-    // MRG: lane item i = (row i >> 1, dim pair lane + 64 (i & 1)) of this wave's 256 dims
-    // (2 heads): every split's (m, l, O pair) loaded here, merged after the weight prefetch
+    // MRG: lane = 4 consecutive dims (kbeg + 4 lane: lanes 0-31 the wave's first head, 32-63 its
+    // second) of each row m < 2: every split's (m, l, O quad) loaded here (3 loads per split and row),
+    // merged after the weight prefetch
     constexpr int NS = MRG ? MRG : 1;
-    float mm[MRG ? 4 : 1][NS], ml[MRG ? 4 : 1][NS];
-    float2 mo[MRG ? 4 : 1][NS];
+    float mm[MRG ? 2 : 1][NS], ml[MRG ? 2 : 1][NS];
+    float4 mo[MRG ? 2 : 1][NS];
     if constexpr (MRG) {
         const int G = (K >> 7) / mhkv;
+        const int k = kbeg + 4 * lane;
+        const int h = k >> 7, d = k & 127, g = h / G, j = h - g * G;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = min(i >> 1, M - 1);
-            const int k = kbeg + 2 * (lane + 64 * (i & 1));
-            const int h = k >> 7, d = k & 127, g = h / G, j = h - g * G;
+        for (int i = 0; i < 2; ++i) {
+            const int m = min(i, M - 1);
             const float* base = mw + ((size_t)m * mhkv + g) * MRG * GF_AT_STR;
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) {
                 mm[i][sp] = base[sp * GF_AT_STR + j];
                 ml[i][sp] = base[sp * GF_AT_STR + GF_AT_G + j];
-                mo[i][sp] = *reinterpret_cast<const float2*>(base + sp * GF_AT_STR + 2 * GF_AT_G + j * 128 + d);
+                mo[i][sp] = *reinterpret_cast<const float4*>(base + sp * GF_AT_STR + 2 * GF_AT_G + j * 128 + d);
             }
         }
     }
+    // mode 3: the position word (scalar, waited below with the skip word) and the lane's RoPE pair
+    int posv = 0;
+    float2 rcs = make_float2(0.f, 0.f);
     bf16_t rv[4] = {0, 0, 0, 0};                                     // residual x of the epilogue
     const int t = w;                                                 // wave w finishes tile w
     const int n_out = (nt0 + t) * 16 + ln;
@@ -783,8 +817,19 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     // the skip word: a scalar load issued here, after the prologue loads and the weight prefetch
-    // (every load above is in bounds; nothing is written yet)
-    if (ld_word_here(skip)) {
+    // (every load above is in bounds; nothing is written yet); mode 3 reads the position word in the
+    // same round trip and issues its (cos, sin) load, which lands during the weight stream
+    int skv;
+    if constexpr (MODE == 3) {
+        ld_words_here(skip, qk.pos, skv, posv);
+        posv = min(max(posv, 0), qk.Smax - 1);
+        const int nq = (qk.H + 2 * qk.Hkv) * 128;      // (N) columns [0, H*128) q, then k, then v
+        const int ncol = min((nt0 + w) * 16 + ln, nq - 1);
+        rcs = *reinterpret_cast<const float2*>(qk.freqs + (size_t)posv * 128 + 2 * ((ncol & 127) >> 1));
+    } else {
+        skv = ld_word_here(skip);
+    }
+    if (skv) {
         // (the prologue / epilogue loads too: sunk below this test they would queue behind the
         // weight prefetch and drain it when waited for)
 #pragma unroll
@@ -804,11 +849,14 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
         }
         if constexpr (MRG) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int sp = 0; sp < NS; ++sp)
-                    asm volatile("" ::"v"(mm[i][sp]), "v"(ml[i][sp]), "v"(mo[i][sp].x), "v"(mo[i][sp].y));
+                for (int sp = 0; sp < NS; ++sp) {
+                    asm volatile("" ::"v"(mm[i][sp]), "v"(ml[i][sp]));
+                    keep_live(mo[i][sp]);
+                }
         }
+        if constexpr (MODE == 3) asm volatile("" ::"v"(rcs.x), "v"(rcs.y));
         if constexpr (MODE == 2) asm volatile("" ::"v"((int)rv[0]), "v"((int)rv[1]), "v"((int)rv[2]), "v"((int)rv[3]));
         return;
     }
@@ -858,33 +906,33 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     }
     if constexpr (MRG) {
         // k_attn_combine's arithmetic, split by split in order (fp32, no contraction)
-        uint32_t* xsw = reinterpret_cast<uint32_t*>(xs);
+        uint2* xsw = reinterpret_cast<uint2*>(xs);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 2; ++i) {
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) {
-                u32x4 t = {__float_as_uint(mm[i][sp]), __float_as_uint(ml[i][sp]), __float_as_uint(mo[i][sp].x),
-                           __float_as_uint(mo[i][sp].y)};
-                asm volatile("" : "+v"(t));               // no merge arithmetic above the weight prefetch
-                mm[i][sp] = __uint_as_float(t[0]);
-                ml[i][sp] = __uint_as_float(t[1]);
-                mo[i][sp] = make_float2(__uint_as_float(t[2]), __uint_as_float(t[3]));
+                float2 t2 = make_float2(mm[i][sp], ml[i][sp]);
+                asm volatile("" : "+v"(t2.x), "+v"(t2.y), "+v"(mo[i][sp].x), "+v"(mo[i][sp].y), "+v"(mo[i][sp].z),
+                             "+v"(mo[i][sp].w));      // no merge arithmetic above the weight prefetch
+                mm[i][sp] = t2.x;
+                ml[i][sp] = t2.y;
             }
             float Mx = -INFINITY;
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) Mx = fmaxf(Mx, mm[i][sp]);
-            float L = 0.f, o0 = 0.f, o1 = 0.f;
+            float L = 0.f, o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) {
                 const float c = (mm[i][sp] == -INFINITY) ? 0.f : __expf(mm[i][sp] - Mx);
                 L += ml[i][sp] * c;
                 o0 += mo[i][sp].x * c;
                 o1 += mo[i][sp].y * c;
+                o2 += mo[i][sp].z * c;
+                o3 += mo[i][sp].w * c;
             }
             const float inv = 1.0f / L;
-            const int m = i >> 1;
-            const int k = kbeg + 2 * (lane + 64 * (i & 1));
-            if (m < M) xsw[(m * GF_XS + k) >> 1] = pack2(o0 * inv, o1 * inv);
+            const int k = kbeg + 4 * lane;
+            if (i < M) xsw[(i * GF_XS + k) >> 2] = make_uint2(pack2(o0 * inv, o1 * inv), pack2(o2 * inv, o3 * inv));
         }
         // each wave reads back only the dims it wrote (its own K range): no workgroup barrier
     }
@@ -909,7 +957,9 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
             }
         }
         __builtin_amdgcn_sched_barrier(0);
+        if (ls == 0) ZK_GF_STAMP(1);
     }
+    ZK_GF_STAMP(2);
 #pragma unroll
     for (int tt = 0; tt < NTW; ++tt) red[w][tt][lane] = acc[tt];
     __syncthreads();
@@ -921,6 +971,7 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
 #pragma unroll
         for (int i = 0; i < 4; ++i) sum[i] = sum[i] + o[i];
     }
+    ZK_GF_STAMP(3);
     if (MODE == 1) {
         const int F = N / 2;
         const int f = (nt0 + t) * 8 + (ln & 7);
@@ -932,6 +983,32 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
             if (ln < 8 && m < M && f < F) {
                 const float sl = round_bf(other / (1.0f + expf(-other)));
                 Cb[(size_t)m * F + f] = f2bf(mine * sl);
+            }
+        }
+        return;
+    }
+    if constexpr (MODE == 3) {
+        const int Hq = qk.H * 128, Hk = qk.Hkv * 128;
+        const int d = n_out & 127;
+        const bool even = (d & 1) == 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float mine = round_bf(sum[i]);
+            const float other = __shfl_xor(mine, 1, 64);      // the pair's other dim (lane ln ^ 1)
+            const int m = lg * 4 + i;
+            if (m >= M || n_out >= N) continue;
+            // (a, b) = dims (2j, 2j+1): o0 = a c - b s, o1 = b c + a s (attn_decode_wg's prologue)
+            const float a = even ? mine : other, b = even ? other : mine;
+            const float rot = even ? __fsub_rn(__fmul_rn(a, rcs.x), __fmul_rn(b, rcs.y))
+                                   : __fadd_rn(__fmul_rn(b, rcs.x), __fmul_rn(a, rcs.y));
+            if (n_out < Hq) {
+                Cb[(size_t)m * Hq + n_out] = f2bf(rot);
+            } else if (n_out < Hq + Hk) {
+                const int g = (n_out - Hq) >> 7;
+                qk.kc[((size_t)m * qk.Hkv + g) * qk.Smax * 128 + k_off(posv, d >> 3) + (d & 7)] = f2bf(rot);
+            } else {
+                const int g = (n_out - Hq - Hk) >> 7;
+                qk.vt[((size_t)m * qk.Hkv + g) * qk.Smax * 128 + v_off(posv, d)] = f2bf(mine);
             }
         }
         return;
@@ -1301,6 +1378,73 @@ extern "C" int zk_gemv_fused(const void* A, long lda, const void* W, int M, int 
     return 0;
 }
 
+// Experiment (tools/microbench.py gemv_warm): a launch that pre-reads into each XCD's L2 the first
+// `steps` weight loads of every wave of a k_gemv_f launch of the given layout (same grid, same
+// workgroup -> tile / K-range map and per-lane addresses), by LDS-DMA into a sink.
+template <int NTW, bool HALF, int NW>
+__global__ __launch_bounds__(64 * NW) void k_gemv_warm(const bf16_t* __restrict__ W, int N, int K, int steps) {
+    __shared__ __attribute__((aligned(16))) char sink[1024];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ln = lane & 15;
+    const int nt0 = HALF ? (blockIdx.x >> 1) : blockIdx.x * NTW;
+    const int half = HALF ? (blockIdx.x & 1) : 0;
+    const bool wl = !HALF || ((ln >> 3) == half);
+    constexpr int KPL = HALF ? 2 : 1;
+    const int ntiles = (N + 63) / 64 * 4;
+    const int kbeg = w * (K / NW);
+    const int lsrc = wl ? lane * 8 : 512 + (lane ^ 8) * 8;
+    void* snk = sink;
+    for (int tt = 0; tt < NTW; ++tt) {
+        const bf16_t* p = W + ((size_t)min(nt0 + tt, ntiles - 1) * (K >> 5) + (kbeg >> 5)) * 512 + lsrc;
+        for (int ls = 0; ls < steps; ++ls)
+            __builtin_amdgcn_global_load_lds((const void*)(p + (size_t)ls * 512 * KPL), snk, 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+extern "C" int zk_gemv_warm(const void* W, int N, int K, int lay, int steps, void* stream) {
+    ZK_REQUIRE(lay >= 0 && lay <= 2 && steps >= 1 && K % 2048 == 0, "zk_gemv_warm: lay %d steps %d K %d", lay, steps,
+               K);
+    const int tiles = (N + 15) / 16;
+    if (lay == 0)
+        hipLaunchKernelGGL((k_gemv_warm<1, true, 8>), dim3(2 * tiles), dim3(512), 0, (hipStream_t)stream,
+                           (const bf16_t*)W, N, K, steps);
+    else if (lay == 1)
+        hipLaunchKernelGGL((k_gemv_warm<1, false, 4>), dim3(tiles), dim3(256), 0, (hipStream_t)stream,
+                           (const bf16_t*)W, N, K, steps);
+    else
+        hipLaunchKernelGGL((k_gemv_warm<2, false, 4>), dim3((tiles + 1) / 2), dim3(256), 0, (hipStream_t)stream,
+                           (const bf16_t*)W, N, K, steps);
+    ZK_CHECK_LAUNCH("zk_gemv_warm");
+    return 0;
+}
+
+#ifdef ZK_GF_PROF
+extern "C" int zk_gf_prof_set(uint64_t* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_gf_prof), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+extern "C" int zk_gemv_qkv_rope(const void* x, const void* W, int M, int H, int Hkv, int hd, const void* ln_w,
+                                const void* ln_b, float eps, void* q_out, void* k_cache, void* vt_cache, int Smax,
+                                const int32_t* pos_dev, const float* freqs, const int32_t* skip_flag, void* stream) {
+    ZK_REQUIRE(M >= 1 && M <= 2, "zk_gemv_qkv_rope: M=%d (1..2)", M);
+    ZK_REQUIRE(hd == 128 && H % Hkv == 0 && H / Hkv <= AT_G, "zk_gemv_qkv_rope: H=%d Hkv=%d hd=%d", H, Hkv, hd);
+    const int K = H * hd, N = (H + 2 * Hkv) * hd;
+    ZK_REQUIRE(K == 2048, "zk_gemv_qkv_rope: d_model %d (2048 only: the LayerNorm prologue)", K);
+    ZK_REQUIRE(x && W && ln_w && ln_b && q_out && k_cache && vt_cache && pos_dev && freqs,
+               "zk_gemv_qkv_rope: null argument");
+    ZK_REQUIRE(Smax > 0 && Smax % 32 == 0, "zk_gemv_qkv_rope: Smax=%d", Smax);
+    const GfQkv qk{(bf16_t*)k_cache, (bf16_t*)vt_cache, pos_dev, freqs, H, Hkv, Smax};
+    constexpr int KS = 64 / ZK_GF_NW, NL = KS, PB = ZK_GF_PFLN;
+    hipLaunchKernelGGL((k_gemv_f<3, true, 1, false, ZK_GF_NW, KS, (NL < PB ? NL : PB), 0, 2>), dim3(N / 16),
+                       dim3(64 * ZK_GF_NW), 0, (hipStream_t)stream, (const bf16_t*)x, (long)K, (const bf16_t*)W, M, N,
+                       K, (const bf16_t*)ln_w, (const bf16_t*)ln_b, eps, nullptr, (bf16_t*)q_out, skip_flag, nullptr, 1,
+                       qk);
+    ZK_CHECK_LAUNCH("zk_gemv_qkv_rope");
+    return 0;
+}
+
 extern "C" int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const void* W, int M, int N, int K,
                                 void* x, const int32_t* skip_flag, void* stream) {
     ZK_REQUIRE(M >= 1 && M <= 2, "zk_gemv_attn_out: M=%d (1..2)", M);
@@ -1316,7 +1460,8 @@ extern "C" int zk_gemv_attn_out(const float* work, int nsplit, int Hkv, const vo
         case 2: ZK_GAO(2); break;
         case 4: ZK_GAO(4); break;
         case 8: ZK_GAO(8); break;
-        default: ZK_REQUIRE(false, "zk_gemv_attn_out: nsplit=%d (2, 4 or 8)", nsplit);
+        case 16: ZK_GAO(16); break;
+        default: ZK_REQUIRE(false, "zk_gemv_attn_out: nsplit=%d (2, 4, 8 or 16)", nsplit);
     }
 #undef ZK_GAO
     ZK_CHECK_LAUNCH("zk_gemv_attn_out");

@@ -98,13 +98,13 @@ def attn_splits_for(R: int, Hkv: int, smax: int, target_blocks: int = 512) -> in
 
 def attn_merge_for(R: int, smax: int) -> int:
     """B = 1 (R = 2 rows): key splits of the decode attention whose partials the out_proj GEMV
-    merges in its prologue (zk_attn_decode_qkv_part + zk_gemv_attn_out) -- more CUs stream the
-    small KV cache without a combine launch or in-launch tickets. 0 = unsplit attention."""
+    merges in its prologue (zk_attn_decode_q_part + zk_gemv_attn_out) -- more CUs stream the
+    small KV cache without a combine launch or in-launch tickets. 0 = unsplit attention. The
+    splits take 32-key slices in turn (4 waves per split), so any count covers any context."""
     if R > 2:
         return 0
-    n = min(ATTN_MERGE_DEFAULT, smax // 128)
-    for v in (8, 4, 2):
-        if n >= v:
+    for v in (16, 8, 4, 2):
+        if ATTN_MERGE_DEFAULT >= v and smax >= 128:
             return v
     return 0
 
@@ -163,6 +163,20 @@ class HipBackbone:
         merge = ws.get("attn_merge", 0)
         for i, L in enumerate(self.layers):
             kc, vt = self._kv(ws, i)
+            if merge and not self.rope_neox:
+                # B = 1: RoPE + KV write in the in_proj epilogue (q -> y), prologue-free attention over
+                # 32-key slices, partials merged by the out_proj GEMV
+                call("zk_gemv_qkv_rope", ptr(x), ptr(L["wqkv"]), R, H, Hk, hd, ptr(L["ln1_w"]), ptr(L["ln1_b"]),
+                     c.eps, ptr(y), ptr(kc), ptr(vt), ws["smax"], ptr(scal[1:2]), ptr(self.freqs), skip, stream)
+                call("zk_attn_decode_q_part", ptr(y), ptr(kc), ptr(vt), R, H, Hk, hd, ws["smax"], 1, ptr(scal[1:2]),
+                     ptr(ws["attn_work"]), merge, skip, stream)
+                call("zk_gemv_attn_out", ptr(ws["attn_work"]), merge, Hk, ptr(L["wo"]), R, D, H * hd, ptr(x), skip,
+                     stream)
+                call("zk_gemv_fused", ptr(x), D, ptr(L["fc1"]), R, 2 * Fd, D, 1, ptr(L["ln2_w"]), ptr(L["ln2_b"]),
+                     c.eps, None, ptr(h), skip, stream)
+                call("zk_gemv_fused", ptr(h), Fd, ptr(L["fc2"]), R, D, Fd, 2, None, None, c.eps, None, ptr(x), skip,
+                     stream)
+                continue
             call("zk_gemv_fused", ptr(x), D, ptr(L["wqkv"]), R, Nqkv, D, 0, ptr(L["ln1_w"]), ptr(L["ln1_b"]), c.eps,
                  ptr(part), None, skip, stream)
             if merge:
