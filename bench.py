@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--stub", action="store_true", help="CPU stand-in workload (launcher/reporting tests)")
     ap.add_argument("--graph-steps", type=int, default=None,
                     help="decode steps per hipGraph replay (default: the engine's graph_steps)")
+    ap.add_argument("--dac-overlap", type=int, default=0,
+                    help="1: decode each step's codes to waveforms on a side stream while the next step's generate "
+                         "runs (the DAC's MFMA-bound convs beside the HBM-bound decode); 0: serial")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary measurements after a 1-GPU c3 run (c2, c5, c3 through Zonos.generate)")
     return ap.parse_args()
@@ -390,9 +393,13 @@ class GpuWorkload:
         self.stats = {"gen_s": 0.0, "dac_s": 0.0}
         self.model_name = ("Zonos-v0.1-transformer" if args.model == "transformer"
                            else "Zonos-v0.1-hybrid (assumed geometry)")
+        self.side = torch.cuda.Stream(dev) if args.dac_overlap else None
+        self.dac_events = []
 
     def step(self, i, timed):
         torch, args = self.torch, self.args
+        if self.side is not None:
+            return self._step_overlap(i, timed)
         t0 = time.time()
         from zonos_amd.distributed import generate_sharded
         # the library's sharded generate: this rank's B utterances of the global B x world batch
@@ -413,10 +420,42 @@ class GpuWorkload:
             self.stats["dac_s"] += t2 - t1
         return sum(int(c.shape[1]) for c in codes)
 
+    def _step_overlap(self, i, timed):
+        """--dac-overlap 1: generate on the engine's stream, then this batch's DAC decode enqueued on a side
+        stream, so it runs while the next step's generate does (the last step's DAC is waited for by sync()
+        inside the timed region). DAC time = HIP events on the side stream (its own duration, overlapped)."""
+        torch, args = self.torch, self.args
+        from zonos_amd.distributed import generate_sharded
+        t0 = time.time()
+        codes, allc = generate_sharded(self.eng, self.cond, self.prefix, args.new_tokens, 2.0,
+                                       args.batch * self.world, self.sp, seed=1000 + i, local_input=True,
+                                       coll_device=self.coll_dev, return_local=True, force_full_length=True,
+                                       poll_every=64)
+        assert len(codes) == args.batch and len(allc) == args.batch * self.world
+        main = torch.cuda.current_stream(self.dev)
+        main.synchronize()
+        t1 = time.time()
+        if timed:
+            self.stats["gen_s"] += t1 - t0
+        if self.dac is not None:
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                for c in codes:
+                    c.record_stream(self.side)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(self.side)
+                self.dac.decode_list(codes)
+                e1.record(self.side)
+            if timed:
+                self.dac_events.append((e0, e1))
+        return sum(int(c.shape[1]) for c in codes)
+
     def sync(self):
         self.torch.cuda.synchronize(self.dev)
 
     def report(self, elapsed, args):
+        if self.dac_events:
+            self.stats["dac_s"] = sum(a.elapsed_time(b) for a, b in self.dac_events) / 1e3
         eng = self.eng
         R = 2 * args.batch
         n_dec = args.new_tokens + 8                       # decode steps per generate (max_steps)
@@ -441,6 +480,8 @@ class GpuWorkload:
         return dict(roofline=roof, step_roofline=step_roof, **extra,
                     breakdown={"generate_s_per_step": round(gen_step_s, 3),
                                "dac_s_per_step": round(self.stats["dac_s"] / args.steps, 3),
+                               "dac_overlap": bool(args.dac_overlap),
+                               "dac_exposed_s_per_step": round(max(0.0, elapsed / args.steps - gen_step_s), 3),
                                "dac_precision": self.dac.precision if self.dac is not None else None,
                                "decode_ms_per_token_step": round(dec_ms, 3)})
 
