@@ -17,8 +17,16 @@ def _rms_bar(name, precision):
     """north_star: waveform RMS error <= 1e-4. fp16 operands (the reference's own GPU autocast
     numerics) reach 5.4e-5 on dac_44k; the 16-channel tiny decoder's fp16-operand error is
     intrinsically 1.06e-4 (CPU emulation: oracle with fp16-rounded conv operands, fp64
-    accumulation), so its fp16 bar is 2e-4."""
+    accumulation), so its fp16 bar is 2e-4. Not the signal's amplitude: both fixtures have an RMS
+    of 0.18-0.20; with 16 channels each conv sums 6x fewer fp16-rounded products than the 44.1 kHz
+    decoder's 96-1536, and the rounding errors do not average out. The signal-relative bound
+    (_REL_BAR) holds every fixture to one standard."""
     return 2e-4 if (precision == "fp16" and name == "dac_tiny") else 1e-4
+
+
+# error RMS / signal RMS: fp16 operands <= 1e-3 (>= 60 dB SNR; dac_44k 3e-4, dac_tiny's intrinsic
+# fp16 floor 5.3e-4), the ~fp32-exact modes <= 1e-4
+_REL_BAR = {"fp16": 1e-3, "fp16x3": 1e-4, "fp32": 1e-4}
 
 
 def _dec(name, precision="fp16x3"):
@@ -42,7 +50,10 @@ def test_dac_decode_golden(name, precision):
     ref = torch.from_numpy(d["wav"])
     assert wav.shape == ref.shape
     rms = (wav - ref).pow(2).mean().sqrt().item()
+    rel = rms / ref.pow(2).mean().sqrt().item()
+    print(f"{name} {precision}: RMS error {rms:.3e}, relative to the signal RMS {rel:.3e}")
     assert rms <= _rms_bar(name, precision), rms   # north_star: waveform RMS error <= 1e-4
+    assert rel <= _REL_BAR[precision], rel
     assert (wav - ref).abs().max().item() < (2e-3 if precision == "fp16" else 1e-4)
     if precision != "fp16":
         assert rms <= 1e-5, rms

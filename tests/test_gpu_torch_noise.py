@@ -122,7 +122,10 @@ def test_generate_reference_noise_teacher_forced(name):
     # A codebook-0 decision between EOS and another token whose margin is within the tolerance may
     # go either way on the GPU; it changes that row's EOS state and the number of sampler calls
     # (a resample), i.e. the noise of every later step. Use the first generator seed whose
-    # reference run has no such decision, so every step stays comparable.
+    # reference run has no such decision, so every step stays comparable. The rejected seeds are
+    # counted and bounded: a near-tie is a rare event per run, so needing more than a
+    # few seeds would mean the tolerance, not chance, excludes the runs.
+    rejected = 0
     for seed in range(4321, 4521):
         g = torch.Generator(device=DEV)
         g.manual_seed(seed)
@@ -137,8 +140,11 @@ def test_generate_reference_noise_teacher_forced(name):
                            noise_fn=noise_fn)
         if not _eos_near_tie(tr, tau_ratio):
             break
+        rejected += 1
     else:
         pytest.fail("no generator seed without an EOS near-tie")
+    print(f"{name}: generator seed {seed}, {rejected} seed(s) rejected for an EOS near-tie")
+    assert rejected <= 3, rejected
     off_ref = int(g.get_offset())
     gold = tr["delayed"].long()
     P = c["prefix"].shape[2]
