@@ -207,6 +207,29 @@ def gemm_roofline(eng):
     return dict(unit="us / launch (isolated)", peak_gbs=HBM_PEAK_GBS, per_step_us=round(per_step, 1), **out)
 
 
+def hybrid_gemm_roofline(eng):
+    """c5: the Mamba2 layers' weight GEMMs (in_proj 2048 -> 8512 unsplit, out_proj 4096 -> 2048 split-K) and
+    the slab reduce after out_proj, launched as the hybrid step launches them over the Mamba layers' weights
+    in turn, HIP events; bytes = weights + activation + output once. (The SSM update itself: `roofline`.)"""
+    from zonos_amd._lib import call, ptr
+    ws, c = eng._ws, eng.cfg
+    R, D, di = ws["R"], c.d_model, c.d_inner
+    sp = ws["splits"]
+    nin = c.d_in_proj
+    part, xn = ws["part"], ws["xn"]
+    Ls = [eng.layers[j] for j in eng.mamba_ids]
+    out = {}
+    for name, key, A, N, K, ns in (("mamba_in_proj", "w_in", xn, nin, D, sp["inp"]),
+                                   ("mamba_out_proj", "w_out", ws["ym"], D, di, sp["out"])):
+        def launch(L, A=A, N=N, K=K, ns=ns, key=key):
+            return lambda st: call("zk_gemm_bf16", ptr(A), K, ptr(L[key]), R, N, K, ns, 0, ptr(part), None, None, st)
+        per = _time_launches([launch(L) for L in Ls], reps=2)
+        b = N * K * 2 + R * K * 2 + R * N * 4 * ns
+        out[name] = dict(M=R, N=N, K=K, nsplit=ns, bytes=int(b), us=round(per * 1e6, 2),
+                         frac=round(b / per / 1e9 / HBM_PEAK_GBS, 4))
+    return dict(unit="us / launch (isolated)", peak_gbs=HBM_PEAK_GBS, **out)
+
+
 def _pmc_field(kernel_prefix: str, field: str, **shape):
     """A field of the committed PMC summary entry matching the kernel prefix and shape (or None)."""
     import glob
@@ -590,7 +613,8 @@ def secondary_runs(args, wl, headline_value):
                          heng, wl.cond, wl.prefix, args.new_tokens, 2.0, B, wl.sp, seed=3000 + i,
                          force_full_length=True, poll_every=64),
                          wl.dac, B, args.lc, args.prefix, args.new_tokens, reps=2, warmup=1,
-                         roofline=lambda: mamba_roofline(heng), eng=heng))
+                         roofline=lambda: mamba_roofline(heng), eng=heng),
+                     gemm_roofline=hybrid_gemm_roofline(heng))
     heng.release()
     del heng
     torch.cuda.empty_cache()
