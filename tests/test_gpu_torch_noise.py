@@ -106,6 +106,9 @@ def _eos_near_tie(tr, tau) -> bool:
     return False
 
 
+MAX_REJECTED = {"sampled_cli": 3, "eos_sampled": 12, "sampled_knobs": 3}
+
+
 @pytest.mark.parametrize("name", ["sampled_cli", "eos_sampled", "sampled_knobs"])
 def test_generate_reference_noise_teacher_forced(name):
     """generate() with the reference's noise (Zonos.generate's default): the oracle's generate (the
@@ -123,8 +126,12 @@ def test_generate_reference_noise_teacher_forced(name):
     # go either way on the GPU; it changes that row's EOS state and the number of sampler calls
     # (a resample), i.e. the noise of every later step. Use the first generator seed whose
     # reference run has no such decision, so every step stays comparable. The rejected seeds are
-    # counted and bounded: a near-tie is a rare event per run, so needing more than a
-    # few seeds would mean the tolerance, not chance, excludes the runs.
+    # counted and bounded per fixture. The count is deterministic (torch's generator,
+    # the CPU oracle); MAX_REJECTED holds the measured count plus a margin of two, so a looser
+    # tolerance or a changed fixture that excludes more runs fails here. eos_sampled is the EOS
+    # fixture: every row ends on a sampled EOS and EOS sits in codebook 0's top two on many steps
+    # of every row, so most seeds carry a near-tie somewhere (10 rejected before seed 4331,
+    # profiles/r6_final_gpu_tests.log); the two other fixtures pass within a few seeds.
     rejected = 0
     for seed in range(4321, 4521):
         g = torch.Generator(device=DEV)
@@ -144,7 +151,7 @@ def test_generate_reference_noise_teacher_forced(name):
     else:
         pytest.fail("no generator seed without an EOS near-tie")
     print(f"{name}: generator seed {seed}, {rejected} seed(s) rejected for an EOS near-tie")
-    assert rejected <= 3, rejected
+    assert rejected <= MAX_REJECTED[name], (name, rejected)
     off_ref = int(g.get_offset())
     gold = tr["delayed"].long()
     P = c["prefix"].shape[2]
