@@ -24,9 +24,10 @@ pytestmark = pytest.mark.gpu
 
 # fp32 CFG logits: the engine and the reference round the same bf16 intermediates (every GEMM
 # output, LayerNorm, head output) but accumulate in different orders, so individual bf16 values
-# differ by an ulp and CFG (2c - u) triples it. Measured on MI355X: max 0.19 / mean 0.019 (c1),
-# max 0.14 / mean 0.028 (c2).
-LOGIT_MAX, LOGIT_MEAN = 0.4, 0.04
+# differ by an ulp and CFG (2c - u) triples it. Measured on MI355X: max 0.25 / mean 0.019 (c1, the max
+# at step 128), max 0.14 / mean 0.028 (c2), max 0.152 / mean 0.028 (c3), max 0.156 / mean 0.027 (c4)
+# (profiles/r6_fullwidth_every_decision.log); the bars keep ~30 % above the largest.
+LOGIT_MAX, LOGIT_MEAN = 0.32, 0.036
 # decision-space tolerance (test_gpu_generate.py): a logit error e moves the unified sampler's
 # log(p1/q1) - log(p2/q2) by up to e * (linear + conf * ln V) / T
 TAU_LOGIT = 0.3
@@ -95,6 +96,37 @@ def _forced_run(name):
     return c, got
 
 
+def _sampler_on_engine_logits(c, got, steps):
+    """The oracle's sampler (zonos_ref.sample, the loop's logit masks of zonos_ref.forced_steps) on the
+    engine's raw CFG logits of each recorded step, keyed noise (seed, step, draw 0, row_base + u) and the
+    forced history; returns (decisions, [(step, utt, cb, engine, oracle)] that differ)."""
+    from oracle import zonos_ref
+    from oracle.philox import exp_noise
+    EOS = zonos_ref.EOS
+    P, rb = c["P"], int(c["row_base"])
+    hist = c["history"]
+    spk = {k: v for k, v in CLI_SP.items() if k != "repetition_penalty"}
+    rp = float(CLI_SP["repetition_penalty"])
+    n, bad = 0, []
+    for s in steps:
+        raw, tok = got[s]
+        off = P + 1 + s
+        for i, u in enumerate(c["utts"]):
+            lg = torch.from_numpy(raw[i:i + 1].copy())
+            if s > 0:
+                lg[:, 1:, EOS] = -torch.inf
+                lg[:, 0, EOS] -= torch.log(torch.tensor(1024.0))
+            lg[:, 0, EOS] = -torch.inf                      # force_full_length (benchmark mode)
+            q = torch.from_numpy(exp_noise(FULL_SEED, s, 0, 1, lg.shape[1], lg.shape[2], rb + int(u)))
+            t = zonos_ref.sample(lg, q, generated_tokens=hist[int(u):int(u) + 1, :, :off] if s > 0 else None,
+                                 repetition_penalty=torch.full((1,), rp), **spk)[0, :, 0]
+            for k in range(lg.shape[1]):
+                n += 1
+                if int(t[k]) != int(tok[i, k]):
+                    bad.append((s, int(u), k, int(tok[i, k]), int(t[k])))
+    return n, bad
+
+
 @pytest.mark.parametrize("name", ["c2", "c3", "c4"])
 def test_full_teacher_forced_logits_and_tokens(name):
     c, got = _forced_run(name)
@@ -119,6 +151,12 @@ def test_full_teacher_forced_logits_and_tokens(name):
     frac = skipped / (checked + skipped)
     print(f"{name}: logits max/mean |d| per step {errs}; decisions checked {checked} skipped {skipped} "
           f"({100 * frac:.1f} %, margin <= {tau:.2f}), mismatches {mism[:5]}")
+    # every decision, skipped ones included: the engine's token is exactly what the reference's
+    # sampler (the oracle, pinned to it by the sampler fixtures) draws from the ENGINE's own logits
+    # with the same noise and history -- so the only difference left is the logits' bounded error
+    n_all, resampled_mism = _sampler_on_engine_logits(c, got, steps)
+    print(f"{name}: reference sampler on the engine's logits: {n_all} decisions, {len(resampled_mism)} differ")
+    assert not resampled_mism, resampled_mism[:10]
     assert max(e[0] for e in errs) < LOGIT_MAX and max(e[1] for e in errs) < LOGIT_MEAN, errs
     assert not mism, mism[:10]
     # CLI sampling = argmax(probs / Exp(1) noise): on near-flat random-weight distributions the
