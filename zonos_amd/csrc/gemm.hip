@@ -692,6 +692,15 @@ constexpr int GF_AT_G = AT_G, GF_AT_STR = AT_STR;    // the partials layout of a
 static_assert(GF_AT_STR == 2 * GF_AT_G + GF_AT_G * 128, "attention partials layout");
 // XR: rows the LDS activation image holds (2 for B = 1, 16 otherwise): a 16-row image is 66 KB and
 // caps the LayerNorm-prologue GEMVs at 2 workgroups per CU; the 2-row image (8 KB) does not.
+// XC (ZK_GF_XC, B = 1 GEMVs without a LayerNorm or merge prologue: fc2): the activation rows are copied
+// into the LDS image once per wave -- each wave its own K range, 4 x 16 B per lane at K = 8192 -- instead
+// of being re-loaded from L2 beside every weight load (two 16-B-per-lane loads per weight piece, 16 lanes
+// per row for the 2 real rows: 2/3 of the wave's load instructions). Same operands, same MFMA order:
+// bit-identical. A pure-stream probe of the fc2 shape: 6.45 -> 7.01 us per launch with those loads
+// (profiles/r6_stream_order_probe.txt).
+#ifndef ZK_GF_XC
+#define ZK_GF_XC 1
+#endif
 #ifndef ZK_GF_OCC2
 #define ZK_GF_OCC2 1               // min waves per SIMD the B = 1 (XR = 2) instantiations are sized for
 #endif
@@ -722,13 +731,17 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     static_assert(!LN || KS * NW * 32 == 2048, "LN prologue: K = 2048");
     static_assert(!MRG || (!LN && NW == 8 && KS * NW * 32 == 2048), "merge prologue: K = 2048, 8 waves");
     static_assert(NTW <= NW, "one finishing wave per tile");
-    constexpr bool XS = LN || MRG;                                   // activation from LDS
+    constexpr bool XC = ZK_GF_XC && XR == 2 && !LN && !MRG;          // activation copied to LDS (see above)
+    constexpr bool XS = LN || MRG || XC;                             // activation from LDS
+    constexpr int XSTR = XC ? NW * KS * 32 + 8 : GF_XS;              // LDS image row stride (bf16)
+    constexpr int XCN = XC ? KS * 32 * 2 / 512 : 1;                  // XC: 16-B loads per lane (2 rows)
+    static_assert(!XC || (KS * 32 * 2) % 512 == 0, "XC: whole 512-element load rounds per wave");
     constexpr int KPL = HALF ? 2 : 1;                                // k-steps per weight load
     constexpr int NL = KS / KPL;                                     // weight loads per wave and tile
     static_assert(NL * KPL == KS, "HALF pairs k-steps");
     constexpr int MR = (XR + NW - 1) / NW;                           // LN rows per wave
     static_assert(!MRG || XR == 2, "merge prologue: M <= 2");
-    __shared__ __attribute__((aligned(16))) uint4 xs[XS ? XR * GF_XS / 8 : 1];
+    __shared__ __attribute__((aligned(16))) uint4 xs[XS ? XR * XSTR / 8 : 1];
     __shared__ __attribute__((aligned(16))) f32x4 red[NW][NTW][64];
 
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -757,6 +770,15 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
                 xv[rr][j] = *reinterpret_cast<const uint4*>(A + (size_t)min(w + NW * rr, M - 1) * lda + lane * 8 + j * 512);
+    }
+    // XC: element e = 512 j + 8 lane of the wave's 2-row image (row e / (K / NW), column kbeg + e % (K / NW))
+    uint4 xc[XCN];
+    if constexpr (XC) {
+#pragma unroll
+        for (int j = 0; j < XCN; ++j) {
+            const int e = j * 512 + lane * 8, row = e / (KS * 32), col = e % (KS * 32);
+            xc[j] = *reinterpret_cast<const uint4*>(A + (size_t)min(row, M - 1) * lda + kbeg + col);
+        }
     }
     // MRG: lane = 4 consecutive dims (kbeg + 4 lane: lanes 0-31 the wave's first head, 32-63 its
     // second) of each row m < 2: every split's (m, l, O quad) loaded here (3 loads per split and row),
@@ -856,6 +878,10 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
                     keep_live(mo[i][sp]);
                 }
         }
+        if constexpr (XC) {
+#pragma unroll
+            for (int j = 0; j < XCN; ++j) keep_live(xc[j]);
+        }
         if constexpr (MODE == 3) asm volatile("" ::"v"(rcs.x), "v"(rcs.y));
         if constexpr (MODE == 2) asm volatile("" ::"v"((int)rv[0]), "v"((int)rv[1]), "v"((int)rv[2]), "v"((int)rv[3]));
         return;
@@ -899,10 +925,20 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
 #pragma unroll
                 for (int e = 0; e < 8; ++e)
                     o[e] = __fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(xf[8 * j + e], rstd), nb), wf[e]), bf[e]);
-                *reinterpret_cast<uint4*>(xsb + m * GF_XS + lane * 8 + j * 512) = pack8(o);
+                *reinterpret_cast<uint4*>(xsb + m * XSTR + lane * 8 + j * 512) = pack8(o);
             }
         }
         __syncthreads();
+    }
+    if constexpr (XC) {
+        // each wave writes (and later reads) only its own K range: no workgroup barrier
+        bf16_t* xsb = reinterpret_cast<bf16_t*>(xs);
+#pragma unroll
+        for (int j = 0; j < XCN; ++j) {
+            opaque(xc[j]);
+            const int e = j * 512 + lane * 8, row = e / (KS * 32), col = e % (KS * 32);
+            *reinterpret_cast<uint4*>(xsb + row * XSTR + kbeg + col) = xc[j];
+        }
     }
     if constexpr (MRG) {
         // k_attn_combine's arithmetic, split by split in order (fp32, no contraction)
@@ -932,7 +968,7 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
             }
             const float inv = 1.0f / L;
             const int k = kbeg + 4 * lane;
-            if (i < M) xsw[(i * GF_XS + k) >> 2] = make_uint2(pack2(o0 * inv, o1 * inv), pack2(o2 * inv, o3 * inv));
+            if (i < M) xsw[(i * XSTR + k) >> 2] = make_uint2(pack2(o0 * inv, o1 * inv), pack2(o2 * inv, o3 * inv));
         }
         // each wave reads back only the dims it wrote (its own K range): no workgroup barrier
     }
@@ -940,7 +976,7 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     f32x4 acc[NTW];
 #pragma unroll
     for (int tt = 0; tt < NTW; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bf16_t* xrow = reinterpret_cast<const bf16_t*>(xs) + mrow * GF_XS + kbeg + lg * 8;
+    const bf16_t* xrow = reinterpret_cast<const bf16_t*>(xs) + mrow * XSTR + kbeg + lg * 8;
 #pragma unroll
     for (int ls = 0; ls < NL; ++ls) {
         if (ls + PF < NL) issue(ls + PF, (ls + PF) % U);
