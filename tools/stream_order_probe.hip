@@ -6,6 +6,8 @@
 //   mode 1: wave (b, w) starts at piece (b * 8 + w) % 16 and wraps (same bytes, rotated start)
 //   mode 2: pieces interleaved across waves (piece l of wave g at (l * nwaves + g) KB): at any time
 //           all waves read neighbouring KBs
+//   mode 4: interleaved across the waves of a workgroup only (piece l of wave w of workgroup b at
+//           b * 128 KB + (l * 8 + w) KB): the k-step assignment a GEMV could change without a new layout
 //   mode 3: mode 0 + the B = 1 fc2 GEMV's activation loads: per weight piece two 16-B-per-lane loads
 //           of a 2 x 8192 bf16 activation (L2-resident; 16 lanes per row, so 2 distinct rows)
 // Each launch reads a different copy of the image (LAYERS copies, far beyond L2 + MALL), as a decode
@@ -32,6 +34,7 @@ __global__ __launch_bounds__(64 * NW) void k_stream(const u32x4* __restrict__ im
         long kb;
         if constexpr (MODE == 0 || MODE == 3) kb = (long)g * NL + l;
         else if constexpr (MODE == 1) kb = (long)g * NL + (l + g) % NL;
+        else if constexpr (MODE == 4) kb = (long)b * NW * NL + l * NW + w;
         else kb = (long)l * (NWG * NW) + g;
         return img + kb * 64 + lane;
     };
@@ -92,7 +95,8 @@ int main(int argc, char** argv) {
                 if (mode == 0) hipLaunchKernelGGL(k_stream<0>, dim3(NWG), dim3(64 * NW), 0, 0, img, out, (unsigned long long*)nullptr, act);
                 else if (mode == 1) hipLaunchKernelGGL(k_stream<1>, dim3(NWG), dim3(64 * NW), 0, 0, img, out, (unsigned long long*)nullptr, act);
                 else if (mode == 2) hipLaunchKernelGGL(k_stream<2>, dim3(NWG), dim3(64 * NW), 0, 0, img, out, (unsigned long long*)nullptr, act);
-                else hipLaunchKernelGGL(k_stream<3>, dim3(NWG), dim3(64 * NW), 0, 0, img, out, (unsigned long long*)nullptr, act);
+                else if (mode == 3) hipLaunchKernelGGL(k_stream<3>, dim3(NWG), dim3(64 * NW), 0, 0, img, out, (unsigned long long*)nullptr, act);
+                else hipLaunchKernelGGL(k_stream<4>, dim3(NWG), dim3(64 * NW), 0, 0, img, out, (unsigned long long*)nullptr, act);
             }
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
@@ -100,12 +104,12 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         return ms * 1000.f / (reps * layers);
     };
-    for (int m = 0; m < 4; ++m) run(m);                                  // warm-up
-    const char* names[4] = {"0 contiguous (product order)", "1 rotated start", "2 interleaved across waves", "3 mode 0 + activation loads"};
+    for (int m = 0; m < 5; ++m) run(m);                                  // warm-up
+    const char* names[5] = {"0 contiguous (product order)", "1 rotated start", "2 interleaved across waves", "3 mode 0 + activation loads", "4 interleaved within a workgroup"};
     printf("# %d workgroups x %d waves x %d KB, %d loads in flight per wave, %d image copies of %.1f MB (us per launch, back to back)\n",
            NWG, NW, NL, PF, layers, img_bytes / 1e6);
     for (int round = 0; round < 3; ++round)
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < 5; ++m) {
             const float us = run(m);
             printf("mode %-30s %7.2f us  %6.2f TB/s\n", names[m], us, img_bytes / us / 1e6);
         }

@@ -701,6 +701,9 @@ static_assert(GF_AT_STR == 2 * GF_AT_G + GF_AT_G * 128, "attention partials layo
 #ifndef ZK_GF_XC
 #define ZK_GF_XC 1
 #endif
+#ifndef ZK_GF_LNW
+#define ZK_GF_LNW 1
+#endif
 #ifndef ZK_GF_OCC2
 #define ZK_GF_OCC2 1               // min waves per SIMD the B = 1 (XR = 2) instantiations are sized for
 #endif
@@ -758,8 +761,10 @@ __global__ __launch_bounds__(64 * NW, XR == 2 ? ZK_GF_OCC2 : 1) void k_gemv_f(co
     // to be waited for without draining it. The empty asm with a memory clobber + sched_barrier
     // keep the compiler from moving these loads behind the prefetch.
     constexpr int NJ = LN ? 4 : 1;                                   // 16-B chunks per lane per row
-    uint4 xv[LN ? MR : 1][NJ], wv[NJ], bv[NJ];
-    if constexpr (LN) {
+    uint4 xv[LN ? MR : 1][NJ] = {}, wv[NJ] = {}, bv[NJ] = {};
+    // ZK_GF_LNW (B = 1): only the waves that normalise a row (w < M) load the row and the LayerNorm
+    // weights; the others issue nothing before their weight prefetch (wave-uniform branch)
+    if constexpr (LN) if (!(ZK_GF_LNW && XR == 2 && MR == 1) || w < M) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             wv[j] = *reinterpret_cast<const uint4*>(lnw + lane * 8 + j * 512);
