@@ -292,6 +292,9 @@ __global__ __launch_bounds__(LN_NT) void k_resid_ln_var(const float* part, int n
 // NS > 0: exactly NS slabs (only real slabs loaded); NS = 0: nsplit <= RL_MAXS with clamped loads
 // WARM: a ninth wave warms the next GEMM's first weight chunks into L2 (warm.h) and keeps the
 // block's barrier count (two per row) without waiting for its loads.
+#ifndef ZK_RL_DEFER
+#define ZK_RL_DEFER 1              // step word tested after the row's loads are issued (see below)
+#endif
 template <int NS, bool WARM = false>
 __global__ __launch_bounds__(WARM ? 576 : 512) void k_resid_ln_d2k512(const float* part, int nsplit, const bf16_t* x_in,
                                                          const bf16_t* w, const bf16_t* b, float eps, int rows,
@@ -300,7 +303,8 @@ __global__ __launch_bounds__(WARM ? 576 : 512) void k_resid_ln_d2k512(const floa
                                                          int wgz, int wch) {
     constexpr int D = 2048;
     __shared__ float red[16];
-    if (skip && *skip) return;
+    if (!ZK_RL_DEFER || (WARM && threadIdx.x >= 512))
+        if (skip && *skip) return;
     if (WARM && threadIdx.x >= 512) {
         __shared__ __attribute__((aligned(16))) char sink[1024];
         warm_units(wW, wK, wgx, wgz, wch, blockIdx.x, gridDim.x, 0, 1, threadIdx.x & 63, sink);
@@ -321,6 +325,17 @@ __global__ __launch_bounds__(WARM ? 576 : 512) void k_resid_ln_d2k512(const floa
 #pragma unroll
     for (int sp = 0; sp < NL; ++sp)
         a0[sp] = *reinterpret_cast<const float4*>(p + (size_t)(NS ? sp : min(sp, nsplit - 1)) * slab + c0);
+    if constexpr (ZK_RL_DEFER) {
+        // the step word after the row's loads (all in bounds): its round trip overlaps theirs
+        if (ld_word_here(skip)) {
+            keep_live(w0);
+            keep_live(b0);
+            keep_live(x0);
+#pragma unroll
+            for (int sp = 0; sp < NL; ++sp) keep_live(a0[sp]);
+            return;
+        }
+    }
     float acc[4] = {a0[0].x, a0[0].y, a0[0].z, a0[0].w};
 #pragma unroll
     for (int sp = 1; sp < NL; ++sp)

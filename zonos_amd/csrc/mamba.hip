@@ -145,6 +145,9 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step(
 #ifndef ZK_MB_PD
 #define ZK_MB_PD 1                   // heads' state slices in flight
 #endif
+#ifndef ZK_MB_DEFER
+#define ZK_MB_DEFER 1                // k_mamba_step_g / k_gated_norm test the step word after their first loads
+#endif
 #ifndef ZK_MB_NT
 #define ZK_MB_NT 3                   // non-temporal SSM state loads (1) / stores (2): c5 decode 4.42 -> 4.34 ms (the stores; loads alone 4.47-4.49)
 #endif
@@ -175,7 +178,8 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
     constexpr int NIT = (NI + MB_THREADS - 1) / MB_THREADS;
     static_assert(TPP * HP == MB_THREADS && EPT * TPP == DS && EPT % 8 == 0, "tile");
     __shared__ float s_x[NX], s_z[NX], s_B[DS], s_C[DS], s_dt[HG];
-    if (skip && *skip) return;
+    if (!ZK_MB_DEFER)
+        if (skip && *skip) return;
     const int h0 = blockIdx.x * HG, r = blockIdx.y;
     const int conv_dim = di + 2 * DS;
     const int ncol = 2 * di + 2 * DS + nh;
@@ -230,6 +234,24 @@ __global__ __launch_bounds__(MB_THREADS) void k_mamba_step_g(
     };
 #pragma unroll
     for (int hh = 0; hh < PD; ++hh) load_state(hh, hh);
+    if constexpr (ZK_MB_DEFER) {
+        // the step word once the prologue and the first state slices are in flight (every load above
+        // is in bounds; nothing is written before this test)
+        if (ld_word_here(skip)) {
+#pragma unroll
+            for (int k = 0; k < NIT; ++k) {
+#pragma unroll
+                for (int g = 0; g < GS; ++g) asm volatile("" ::"v"(sv[k][g]));
+                asm volatile("" ::"v"(cst[k].x), "v"(cst[k].y), "v"(cb[k]));
+                keep_live(cw[k]);
+            }
+#pragma unroll
+            for (int hh = 0; hh < PD; ++hh)
+#pragma unroll
+                for (int v = 0; v < NV; ++v) keep_live(st[hh][v]);
+            return;
+        }
+    }
 
     // ---- prologue arithmetic (the per-item arithmetic of k_mamba_step)
 #pragma unroll
@@ -425,7 +447,8 @@ __global__ __launch_bounds__(MB_THREADS) void k_gated_norm(const float* __restri
                                                            const float* __restrict__ w, float eps,
                                                            bf16_t* __restrict__ out, const int32_t* __restrict__ skip) {
     __shared__ float red[MB_THREADS / 64];
-    if (skip && *skip) return;
+    if (!ZK_MB_DEFER || di > GN_MAXJ * MB_THREADS)
+        if (skip && *skip) return;
     const int row = blockIdx.x;
     const float* gr = g + (size_t)row * di;
     if (di <= GN_MAXJ * MB_THREADS) {
@@ -437,6 +460,13 @@ __global__ __launch_bounds__(MB_THREADS) void k_gated_norm(const float* __restri
             const int j = threadIdx.x + k * MB_THREADS;
             gv[k] = j < di ? gr[j] : 0.f;
             wv[k] = j < di ? w[j] : 0.f;
+        }
+        if constexpr (ZK_MB_DEFER) {
+            if (ld_word_here(skip)) {        // the step word after the row's loads (in bounds)
+#pragma unroll
+                for (int k = 0; k < GN_MAXJ; ++k) asm volatile("" ::"v"(gv[k]), "v"(wv[k]));
+                return;
+            }
         }
         float s = 0.f;
 #pragma unroll
