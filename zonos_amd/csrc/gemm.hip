@@ -246,6 +246,9 @@ constexpr int WS_PF = ZK_WS_PF;  // weight chunks in flight per compute wave: th
 constexpr int WS_PF0 = ZK_WS_PF0; // ... and the split-K slab GEMMs (mode 0): 3 measured faster for the
                                   // in_proj / out_proj / fc2 shapes, 4 for fc1 (profiles/r3s2_gemm_pf_ab.txt)
 constexpr bool WS_NT = ZK_WS_NT; // non-temporal weight loads
+#ifndef ZK_WS_DEFER
+#define ZK_WS_DEFER 0              // k_gemm_ws: step word tested after the first loads (A/B only)
+#endif
 
 
 // k_gemm_ws split-K slab stores (read once by the consumer kernel): non-temporal with ZK_SLAB_NT
@@ -296,8 +299,10 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // (the skip word is tested first here: deferring the test behind the first loads, as k_gemv_f
     // does, measured 0.3-1.2 % slower per c3 step with a vector or a scalar load of the word,
-    // profiles/r3s2_skip_defer_ab.txt)
-    if (skip && *skip) return;
+    // profiles/r3s2_skip_defer_ab.txt; again in round 6, 3.500-3.510 vs 3.473-3.489 ms, while k_resid_ln gained:
+    // profiles/r6_c3_gemm_ws_defer_ab.txt; ZK_WS_DEFER=1 builds that form)
+    if (!ZK_WS_DEFER)
+        if (skip && *skip) return;
     int bx, bz;
     ws_tile(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x, gridDim.z, bx, bz);     // gridDim.y == 1
     constexpr int BNW = 16 * NCW * NG;            // columns per workgroup
@@ -337,6 +342,12 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
         };
         const int pre = min(WS_DA, nchunks);
         for (int c = 0; c < pre; ++c) issue(c);
+        if constexpr (ZK_WS_DEFER) {
+            if (ld_word_here(skip)) {           // the LDS-DMA writes land before the workgroup may leave
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                return;
+            }
+        }
         for (int c = 0; c < nchunks; ++c) {
             // barrier c publishes chunk `need` (one chunk ahead, so the compute
             // waves can read chunk c+1's fragments while they multiply chunk c)
@@ -394,6 +405,18 @@ __global__ __launch_bounds__(64 * (NCW + ws_nld<NCW, MT>()), ZK_WS_OCC) void k_g
         for (int g = 0; g < NG; ++g) {
             wr0[g][p] = ldg_w<WS_NT>(wrow[g] + pc * WCH);
             wr1[g][p] = ldg_w<WS_NT>(wrow[g] + pc * WCH + WHALF);
+        }
+    }
+    if constexpr (ZK_WS_DEFER) {
+        if (ld_word_here(skip)) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p)
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    keep_live(wr0[g][p]);
+                    keep_live(wr1[g][p]);
+                }
+            return;
         }
     }
     // activation fragments of the next chunk are read from LDS (register double buffer) while
