@@ -369,7 +369,12 @@ def test_embed_codes():
                                            (2, 2048, 2048, 2, False), (16, 2048, 8192, 2, False),
                                            (1, 2048, 4096, 2, False), (2, 16384, 2048, 1, True),
                                            (9, 16384, 2048, 1, True), (7, 4000, 2048, 0, False),
-                                           (3, 5000, 2048, 0, True), (4, 5000, 8192, 2, False)])
+                                           (3, 5000, 2048, 0, True), (4, 5000, 8192, 2, False),
+                                           # B = 1 (M <= 2): activation staged in LDS per wave (ZK_GF_XC) at
+                                           # every K and layout, LayerNorm loads by the normalising waves only
+                                           (2, 2048, 8192, 2, False), (1, 4000, 2048, 0, False),
+                                           (2, 16384, 4096, 1, False), (2, 9234, 8192, 0, False),
+                                           (1, 16384, 2048, 1, True)])
 def test_gemv_fused(M, N, K, mode, ln):
     """Small-batch GEMV (zk_gemv_fused): LayerNorm prologue, fp32 / SwiGLU / residual epilogues,
     half-tile, one-tile and two-tile layouts, against torch on the CPU at the same rounding points."""
