@@ -238,12 +238,53 @@ struct __attribute__((aligned(16))) AttnSmem {
 // among those 4 waves (__syncthreads in k_attn_decode); `issued` runs right after the first key
 // blocks' loads are in flight and before anything reads the in_proj output or writes anything:
 // it returns true when the launch is to be skipped (generation finished).
-template <bool FUSED, bool NEOX, bool KVNT, bool COMB, class Bar, class Issued>
+// PGS > 0 (FUSED, exactly PGS in_proj slabs): the prologue's slab loads are issued FIRST, then the context
+// word is waited for, then the RoPE row and the first key blocks are requested: the prologue then waits only
+// for its own (older) loads while the key blocks stream, instead of for everything (vmcnt retires in issue
+// order), and the key loop starts while the early key blocks are still arriving.
+template <bool FUSED, bool NEOX, bool KVNT, bool COMB, int PGS, class Bar, class Issued>
 ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, int split, int nsplit, int g, int r,
-                           const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H, int Hkv, int Smax, int ctx,
-                           float* work, float scale, bf16_t* out, const float* part, int gsplit, const float* freqs,
-                           uint32_t* cnt) {
+                           const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H, int Hkv, int Smax, int ctx0,
+                           int cwr, float* work, float scale, bf16_t* out, const float* part, int gsplit,
+                           const float* freqs, uint32_t* cnt) {
     constexpr int HD = 128;
+    static_assert(PGS == 0 || FUSED, "slab pre-loads: the fused prologue");
+    constexpr int NPI = 2;                       // prologue pairs per thread: (G + 2) * 64 <= 384 <= 2 * 256
+    static_assert((AT_G + 2) * (HD / 2) <= NPI * 256, "prologue pairs per thread");
+    float2 psl[PGS > 0 ? NPI : 1][PGS > 0 ? PGS : 1];
+    float2 pcs[PGS > 0 ? NPI : 1];
+    if constexpr (PGS > 0) {
+        const int N = (H + 2 * Hkv) * HD;
+        const size_t slab = (size_t)R * N;
+        const float* prow = part + (size_t)r * N;
+        const int Gq = H / Hkv;
+#pragma unroll
+        for (int it = 0; it < NPI; ++it) {
+            const int pi = min((int)threadIdx.x + 256 * it, (Gq + 2) * (HD / 2) - 1);
+            const int hp = pi / (HD / 2), j = pi % (HD / 2);
+            int d0, d1;
+            rope_dims<NEOX>(j, HD, d0, d1);
+            const int cb = hp < Gq ? (g * Gq + hp) * HD : (hp == Gq ? H * HD + g * HD : (H + Hkv) * HD + g * HD);
+#pragma unroll
+            for (int sl = 0; sl < PGS; ++sl) {
+                if constexpr (NEOX) psl[it][sl] = make_float2(prow[cb + sl * slab + d0], prow[cb + sl * slab + d1]);
+                else psl[it][sl] = *reinterpret_cast<const float2*>(prow + cb + sl * slab + d0);
+            }
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int ctx = min(ctx0 + uni(cwr), Smax);
+    if constexpr (PGS > 0) {
+        const float* fc = freqs + (size_t)(ctx - 1) * HD;
+#pragma unroll
+        for (int it = 0; it < NPI; ++it) {
+            const int pi = min((int)threadIdx.x + 256 * it, (H / Hkv + 2) * (HD / 2) - 1);
+            pcs[it] = *reinterpret_cast<const float2*>(fc + 2 * (pi % (HD / 2)));
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    }
     auto& s_m = sm.s_m;
     auto& s_l = sm.s_l;
     auto& s_o = sm.s_o;
@@ -279,12 +320,23 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
     // patches the new K/V into its registers from LDS instead, so the arithmetic is exactly
     // that of reading the cache. The first key block can therefore be fetched before the prologue.
     const int pos = ctx - 1;
-    const bool early = FUSED && kbw > kb0;
+    // (PGS > 0: both blocks unconditionally, clamped into the cache -- straight-line loads, so the prologue's
+    // wait for its older slab loads is exact and leaves these in flight; an unused block costs 32 KB)
+    const bool early = FUSED && (PGS > 0 || kbw > kb0);
     if (early) {      // the first TWO key blocks are in flight during the prologue
         load_kv<KVNT>(fa, kb, vb, Smax, kb0 * AT_KB + 32 * w, ln, lg);
-        if (!ZK_ATT_TRIM || kb0 + 1 < kbw) load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, last) * AT_KB + 32 * w, ln, lg);
+        if (PGS > 0 || !ZK_ATT_TRIM || kb0 + 1 < kbw)
+            load_kv<KVNT>(fb, kb, vb, Smax, min(kb0 + 1, max(last, kb0)) * AT_KB + 32 * w, ln, lg);
     }
     if (issued()) {          // skip: nothing is written (the loads above are in bounds)
+        if constexpr (PGS > 0) {
+#pragma unroll
+            for (int it = 0; it < NPI; ++it) {
+                asm volatile("" ::"v"(pcs[it].x), "v"(pcs[it].y));
+#pragma unroll
+                for (int sl = 0; sl < PGS; ++sl) asm volatile("" ::"v"(psl[it][sl].x), "v"(psl[it][sl].y));
+            }
+        }
         if (early) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -304,7 +356,33 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
         const float* fc = freqs + (size_t)pos * HD;
         uint16_t* q16 = reinterpret_cast<uint16_t*>(&s_q[0][0]);
         uint16_t* k16 = reinterpret_cast<uint16_t*>(s_kn);
-        for (int pi = threadIdx.x; pi < (G + 2) * (HD / 2); pi += 256) {
+        if constexpr (PGS > 0) {
+#pragma unroll
+            for (int it = 0; it < NPI; ++it) {
+                const int pi = threadIdx.x + 256 * it;
+                if (pi >= (G + 2) * (HD / 2)) break;
+                const int hp = pi / (HD / 2), j = pi % (HD / 2);
+                int d0, d1;
+                rope_dims<NEOX>(j, HD, d0, d1);
+                float a = psl[it][0].x, bb = psl[it][0].y;          // slab_pair's left-to-right sum
+#pragma unroll
+                for (int sl = 1; sl < PGS; ++sl) { a += psl[it][sl].x; bb += psl[it][sl].y; }
+                const float2 cs = pcs[it];
+                a = round_bf(a);
+                bb = round_bf(bb);
+                if (hp <= G) {
+                    const float o0 = __fsub_rn(__fmul_rn(a, cs.x), __fmul_rn(bb, cs.y));
+                    const float o1 = __fadd_rn(__fmul_rn(bb, cs.x), __fmul_rn(a, cs.y));
+                    uint16_t* dst = hp < G ? q16 + hp * HD : k16;
+                    dst[d0] = f2bf(o0);
+                    dst[d1] = f2bf(o1);
+                } else {
+                    s_vn[d0] = f2bf(a);
+                    s_vn[d1] = f2bf(bb);
+                }
+            }
+        }
+        for (int pi = PGS > 0 ? (G + 2) * (HD / 2) : threadIdx.x; pi < (G + 2) * (HD / 2); pi += 256) {
             const int hp = pi / (HD / 2), j = pi % (HD / 2);      // hp < G: q head g*G+hp; G: k; G+1: v
             int d0, d1;
             rope_dims<NEOX>(j, HD, d0, d1);
@@ -573,7 +651,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode_qs(const bf16_t* q, cons
     ZK_ATT_STAMP(5);
 }
 
-template <bool FUSED, bool NEOX, bool KVNT, bool COMB = false>
+template <bool FUSED, bool NEOX, bool KVNT, bool COMB = false, int PGS = 0>
 __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t* kc, bf16_t* vt, int R, int H,
                                                         int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
                                                         float* work, float scale, bf16_t* out, const int32_t* skip,
@@ -583,12 +661,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode(const bf16_t* q, bf16_t*
     // both step scalars in one round trip; the skip word is tested once the first key blocks'
     // loads are in flight (issued -> return), so its latency overlaps theirs
     const int sk = ld_word(skip);
-    // (clamped to the cache: a skipped launch after the last step may see ctx = Smax + 1, and its
-    // first key blocks are loaded before the skip test; every real step has ctx <= Smax)
-    const int ctx = min(ctx0 + uni(ld_word(ctx_dev)), Smax);
-    attn_decode_wg<FUSED, NEOX, KVNT, COMB>(sm, [] { __syncthreads(); }, [sk] { return uni(sk) != 0; }, blockIdx.x,
-                                           gridDim.x, blockIdx.y, blockIdx.z, q, kc, vt, R, H, Hkv, Smax, ctx, work,
-                                           scale, out, part, gsplit, freqs, cnt);
+    // (the context is clamped to the cache: a skipped launch after the last step may see ctx = Smax + 1,
+    // and its first key blocks are loaded before the skip test; every real step has ctx <= Smax)
+    const int cwr = ld_word(ctx_dev);
+    attn_decode_wg<FUSED, NEOX, KVNT, COMB, PGS>(sm, [] { __syncthreads(); }, [sk] { return uni(sk) != 0; },
+                                                blockIdx.x, gridDim.x, blockIdx.y, blockIdx.z, q, kc, vt, R, H, Hkv,
+                                                Smax, ctx0, cwr, work, scale, out, part, gsplit, freqs, cnt);
 }
 
 }  // namespace

@@ -674,6 +674,21 @@ extern "C" int zk_attn_decode(const void* q, const void* k_cache, const void* vt
     return 0;
 }
 
+#ifndef ZK_ATT_PRE
+#define ZK_ATT_PRE 1               // fused decode attention: in_proj slab loads before the key blocks (attn_common.h)
+#endif
+// the fused decode attention instantiation: RoPE form, non-temporal KV loads, in-launch combine, and the
+// slab pre-load form when the in_proj GEMM ran with exactly 4 splits (every c3-c5 decode step)
+template <bool COMB>
+static auto fused_attn_kernel(bool neox, bool kvnt, int gemm_nsplit) {
+    const bool pre = ZK_ATT_PRE && gemm_nsplit == 4;
+    if (pre)
+        return neox ? (kvnt ? k_attn_decode<true, true, true, COMB, 4> : k_attn_decode<true, true, false, COMB, 4>)
+                    : (kvnt ? k_attn_decode<true, false, true, COMB, 4> : k_attn_decode<true, false, false, COMB, 4>);
+    return neox ? (kvnt ? k_attn_decode<true, true, true, COMB, 0> : k_attn_decode<true, true, false, COMB, 0>)
+                : (kvnt ? k_attn_decode<true, false, true, COMB, 0> : k_attn_decode<true, false, false, COMB, 0>);
+}
+
 extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const float* freqs, void* k_cache,
                                   void* vt_cache, int R, int H, int Hkv, int hd, int Smax, int ctx0,
                                   const int32_t* ctx_dev, float* work, int nsplit, void* out, int rope_neox,
@@ -693,8 +708,7 @@ extern "C" int zk_attn_decode_qkv(const float* part, int gemm_nsplit, const floa
     const bf16_t* dbgq = nullptr;
 #endif
     const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
-    auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true> : k_attn_decode<true, true, false>)
-                          : (kvnt ? k_attn_decode<true, false, true> : k_attn_decode<true, false, false>);
+    auto kern = fused_attn_kernel<false>(rope_neox, kvnt, gemm_nsplit);
     hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, dbgq, (bf16_t*)k_cache,
                        (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out, skip, part,
                        gemm_nsplit, freqs, nullptr);
@@ -721,8 +735,7 @@ extern "C" int zk_attn_decode_qkv_part(const float* part, int gemm_nsplit, const
                "zk_attn_decode_qkv_part: bad arguments (gemm_nsplit=%d, max %d)", gemm_nsplit, AT_MAXGS);
     const float scale = 1.0f / sqrtf((float)hd);
     const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
-    auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true> : k_attn_decode<true, true, false>)
-                          : (kvnt ? k_attn_decode<true, false, true> : k_attn_decode<true, false, false>);
+    auto kern = fused_attn_kernel<false>(rope_neox, kvnt, gemm_nsplit);
     hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
                        (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, nullptr, skip, part,
                        gemm_nsplit, freqs, nullptr);
@@ -765,8 +778,7 @@ extern "C" int zk_attn_decode_qkv_sc(const float* part, int gemm_nsplit, const f
                "zk_attn_decode_qkv_sc: bad arguments (gemm_nsplit=%d, max %d)", gemm_nsplit, AT_MAXGS);
     const float scale = 1.0f / sqrtf((float)hd);
     const bool kvnt = (double)R * Hkv * Smax * hd * 4 >= KV_NT_BYTES;
-    auto kern = rope_neox ? (kvnt ? k_attn_decode<true, true, true, true> : k_attn_decode<true, true, false, true>)
-                          : (kvnt ? k_attn_decode<true, false, true, true> : k_attn_decode<true, false, false, true>);
+    auto kern = fused_attn_kernel<true>(rope_neox, kvnt, gemm_nsplit);
     hipLaunchKernelGGL(kern, dim3(nsplit, Hkv, R), dim3(256), 0, (hipStream_t)stream, nullptr, (bf16_t*)k_cache,
                        (bf16_t*)vt_cache, R, H, Hkv, Smax, ctx0, ctx_dev, work, scale, (bf16_t*)out, skip, part,
                        gemm_nsplit, freqs, counters);
