@@ -211,15 +211,23 @@ ZK_DEV void slab_pair_n(const float* p, size_t slab, int ns, int d0, int d1, flo
 
 // ZK_ATT_PROF (profiling builds only): thread 0 of each workgroup writes s_memrealtime stamps
 // [entry, loads issued, prologue done, key loop done, merged, end] to prof[wg * 8 + k].
+// The pointer is read once, at the top of the kernel (ZK_ATT_PROF_PTR, by a scalar load before any data
+// load), so a stamp is a register-sourced store: re-reading the global at each stamp put a vector load
+// behind the key blocks in flight, and the wait for it drained them (the stamps moved the kernel).
 #ifdef ZK_ATT_PROF
+__device__ uint64_t* g_att_prof;
+#define ZK_ATT_PROF_PTR                                                                                     \
+    uint64_t* const zk_pp = reinterpret_cast<uint64_t*>(                                                    \
+        (uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)reinterpret_cast<uintptr_t>(g_att_prof)) | \
+        ((uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(reinterpret_cast<uintptr_t>(g_att_prof) >> 32)) << 32))
 #define ZK_ATT_STAMP(k)                                                                                     \
     do {                                                                                                    \
-        if (threadIdx.x == 0 && g_att_prof)                                                                 \
-            g_att_prof[((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + (k)] =          \
+        if (threadIdx.x == 0 && zk_pp)                                                                      \
+            zk_pp[((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + (k)] =               \
                 __builtin_amdgcn_s_memrealtime();                                                           \
     } while (0)
-__device__ uint64_t* g_att_prof;
 #else
+#define ZK_ATT_PROF_PTR do {} while (0)
 #define ZK_ATT_STAMP(k) do {} while (0)
 #endif
 
@@ -248,6 +256,8 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
                            int cwr, float* work, float scale, bf16_t* out, const float* part, int gsplit,
                            const float* freqs, uint32_t* cnt) {
     constexpr int HD = 128;
+    ZK_ATT_PROF_PTR;
+    ZK_ATT_STAMP(0);
     static_assert(PGS == 0 || FUSED, "slab pre-loads: the fused prologue");
     constexpr int NPI = 2;                       // prologue pairs per thread: (G + 2) * 64 <= 384 <= 2 * 256
     static_assert((AT_G + 2) * (HD / 2) <= NPI * 256, "prologue pairs per thread");
@@ -292,7 +302,6 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
     auto& s_kn = sm.s_kn;
     auto& s_vn = sm.s_vn;
     auto& s_last = sm.s_last;
-    ZK_ATT_STAMP(0);
     const int nkb = (ctx + AT_KB - 1) / AT_KB;
     const int kb0 = (int)((long)split * nkb / nsplit), kb1 = (int)((long)(split + 1) * nkb / nsplit);
     const int G = H / Hkv;
@@ -557,6 +566,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_decode_qs(const bf16_t* q, cons
                                                            int H, int Hkv, int Smax, int ctx0, const int32_t* ctx_dev,
                                                            float* work, float scale, const int32_t* skip) {
     constexpr int HD = 128;
+    ZK_ATT_PROF_PTR;
     __shared__ AttnSmem sm;
     const int split = blockIdx.x, nsplit = gridDim.x, g = blockIdx.y, r = blockIdx.z;
     const int G = H / Hkv;
