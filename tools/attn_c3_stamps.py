@@ -45,6 +45,29 @@ for new in (300, 1300, 2500):
     for i, n in enumerate(names):
         x = rel[:, i]
         print(f"  {n:9s} p10 {q(x, .1):7.2f}  p50 {q(x, .5):7.2f}  p90 {q(x, .9):7.2f}  max {q(x, 1):7.2f}", flush=True)
+    hw = prof.view(-1, 8)[used][:, 6:8].cpu()
+    if int(hw[:, 1].max()) > 0 or int(hw[:, 0].max()) > 0:
+        xcc = (hw[:, 1] & 0xF).long()
+        cu = ((hw[:, 0] >> 8) & 0xF) + 16 * ((hw[:, 0] >> 13) & 0x3) + 64 * ((hw[:, 0] >> 12) & 0x1)
+        loop_end = rel[:, 3]
+        print("  loop end by XCC: " + "  ".join(f"{x}: p50 {q(loop_end[xcc == x], .5):.1f} max {q(loop_end[xcc == x], 1):.1f}"
+                                                for x in range(8) if int((xcc == x).sum()) > 0), flush=True)
+        key = xcc * 1024 + cu
+        same, diff = [], []
+        for k in key.unique():
+            idx = (key == k).nonzero().flatten()
+            if len(idx) == 2:
+                same.append(abs(float(loop_end[idx[0]] - loop_end[idx[1]])))
+        if same:
+            same = torch.tensor(same)
+            print(f"  workgroup pairs sharing a CU: {len(same)}; |loop end difference| p50 {q(same, .5):.1f} max {q(same, 1):.1f} us",
+                  flush=True)
+        cu_end = {}
+        for k in key.unique():
+            cu_end[int(k)] = float(loop_end[key == k].max())
+        ce = torch.tensor(list(cu_end.values()))
+        print(f"  per-CU last loop end ({len(ce)} CUs): p10 {q(ce, .1):.1f} p50 {q(ce, .5):.1f} p90 {q(ce, .9):.1f} max {q(ce, 1):.1f}",
+              flush=True)
     dur = rel[:, 5] - rel[:, 0]
     print(f"  per-workgroup duration p10 {q(dur, .1):.2f} p50 {q(dur, .5):.2f} p90 {q(dur, .9):.2f} max {q(dur, 1):.2f}",
           flush=True)

@@ -226,9 +226,19 @@ __device__ uint64_t* g_att_prof;
             zk_pp[((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + (k)] =               \
                 __builtin_amdgcn_s_memrealtime();                                                           \
     } while (0)
+// slots 6 / 7: HW_ID and XCC_ID of the workgroup's wave 0 (where it ran)
+#define ZK_ATT_HWID()                                                                                       \
+    do {                                                                                                    \
+        if (threadIdx.x == 0 && zk_pp) {                                                                    \
+            const size_t b_ = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8;          \
+            zk_pp[b_ + 6] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                              \
+            zk_pp[b_ + 7] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);                             \
+        }                                                                                                   \
+    } while (0)
 #else
 #define ZK_ATT_PROF_PTR do {} while (0)
 #define ZK_ATT_STAMP(k) do {} while (0)
+#define ZK_ATT_HWID() do {} while (0)
 #endif
 
 // LDS of one attention workgroup (4 waves)
@@ -498,6 +508,7 @@ ZK_DEV void attn_decode_wg(AttnSmem& sm, const Bar& bar, const Issued& issued, i
                 pack2(o0 * inv, o1 * inv);
         }
         ZK_ATT_STAMP(5);
+        ZK_ATT_HWID();
         return;
     }
     float* wp = work + (((size_t)r * Hkv + g) * nsplit + split) * AT_STR;
