@@ -520,6 +520,7 @@ def _timed_config(torch, dev, generate, dac, B, lc, P, new, reps, warmup, roofli
     gen_s = dac_s = 0.0
     frames = 0
     for i in range(warmup + reps):
+        print(f"[bench] secondary rep {i + 1}/{warmup + reps} (B={B}, {new} tokens)", file=sys.stderr, flush=True)
         torch.cuda.synchronize(dev)
         t0 = time.time()
         codes = generate(i)
@@ -652,8 +653,13 @@ def main():
         wl = GpuWorkload(args, rank, world, dist, dev)
         wl.coll_dev = torch.device("cpu") if share else dev
 
+    def progress(msg):      # stderr, rank 0: long runs show they are alive (stdout keeps the one JSON line)
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
     for i in range(args.warmup):
         wl.step(i, False)
+        progress(f"warm-up step {i + 1}/{args.warmup}")
     if dist is not None:
         dist.barrier()
     wl.sync()
@@ -661,6 +667,7 @@ def main():
     frames = 0
     for i in range(args.steps):
         frames += wl.step(args.warmup + i, True)
+        progress(f"timed step {i + 1}/{args.steps}")
     wl.sync()
     if dist is not None:
         dist.barrier()
