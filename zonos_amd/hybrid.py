@@ -27,6 +27,10 @@ from . import _lib
 from ._lib import call, ptr
 from .engine import ATTN_CHUNK, N_CB, VOCAB, HipDecoder, _split_for, attn_splits_for, pack_weights
 
+# split-K of the Mamba in_proj GEMM at decode (k_mamba_step reads the slabs: 1, 2 or 4); unsplit is fastest, again in
+# round 6 after the step-word change: 4.263-4.280 / 4.316-4.317 / 4.585-4.586 ms (profiles/r6_c5_inp_split_ab.txt)
+MAMBA_INP_SPLIT = 1
+
 
 @dataclass
 class HybridEngineConfig:
@@ -374,7 +378,7 @@ class HybridDecoder(HybridBackbone, HipDecoder):
         # profiles/r4s3_hyb_inp_split_ab.txt)
         # (attention out_proj 4-way and the heads unsplit, as the transformer engine: 4.645 vs 4.670 ms)
         splits = dict(qkv=_split_for(Nqkv, D, R), o=_split_for(D, H * hd, R, target_blocks=128),
-                      fc2=_split_for(D, max(Fd, 64), R), heads=1, inp=1, out=_split_for(D, di, R))
+                      fc2=_split_for(D, max(Fd, 64), R), heads=1, inp=MAMBA_INP_SPLIT, out=_split_for(D, di, R))
         part_n = max(Mp * Nqkv, Mp * D, Mp * nin, splits["qkv"] * R * Nqkv, splits["o"] * R * D,
                      splits["fc2"] * R * D, splits["heads"] * R * Nh, splits["inp"] * R * nin, splits["out"] * R * D)
         if c.d_mlp and not Fd:       # a Mamba-block MLP without attention MLPs: its own fc2 split
